@@ -1,0 +1,120 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) against outputs of the reference itself
+(tests/golden, produced by tools/gen_golden.py from /root/reference)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ref_cpu as R
+from itsd.arch import ARCH_A, ARCH_TINY, ARCH_TINY_CFG
+from itsd.weights import synthetic_state_dict
+from itsd.schedule import make_schedule
+
+FP32_EPS_TOL = 1e-4  # max-abs on eps per forward, stated in DESIGN.md
+
+
+def _fw(a, sd):
+    return lambda x, t, labels=None: R.unet_forward(sd, x, t, a.ch, a.ch_mult, a.attn, a.num_res_blocks,
+                                                    labels=labels, cfg=a.cfg)
+
+
+@pytest.mark.parametrize("T,bT", [(1000, 0.02), (1000, 0.028), (3000, 0.02), (10, 0.02)])
+def test_schedule_bitexact(T, bT):
+    g = golden("schedules")
+    tag = f"T{T}_b{bT}"
+    s = R.schedule(1e-4, bT, T)
+    h = make_schedule(1e-4, bT, T)
+    for k in ("betas", "coeff1", "coeff2", "posterior_var", "var"):
+        np.testing.assert_array_equal(s[k].numpy(), g[f"{tag}_{k}"])
+        np.testing.assert_array_equal(getattr(h, k).numpy(), g[f"{tag}_{k}"])
+
+
+def test_tiny_ddpm_eps():
+    g = golden("tiny_ddpm_eps")
+    sd = synthetic_state_dict(ARCH_TINY, 0)
+    with torch.no_grad():
+        eps = _fw(ARCH_TINY, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]))
+        temb = R.time_embedding(sd, torch.from_numpy(g["t"]), ARCH_TINY.ch)
+    np.testing.assert_allclose(temb.numpy(), g["temb"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def test_tiny_cfg_eps():
+    g = golden("tiny_cfg_eps")
+    sd = synthetic_state_dict(ARCH_TINY_CFG, 0)
+    with torch.no_grad():
+        eps = _fw(ARCH_TINY_CFG, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]),
+                                     torch.from_numpy(g["labels"]))
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def test_archA_eps():
+    g = golden("archA_eps")
+    sd = synthetic_state_dict(ARCH_A, 0)
+    with torch.no_grad():
+        eps = _fw(ARCH_A, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]))
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def _traj(a, sd, gname, bT, labels=None, w=0.0):
+    g = golden(gname)
+    T = int(g["T"])
+    s = R.schedule(1e-4, bT, T)
+    noise = torch.from_numpy(g["noise"])
+    f = _fw(a, sd)
+    mf = f if labels is None else R.cfg_eps(lambda x, t, l: f(x, t, l), labels, w)
+    with torch.no_grad():
+        x0 = R.p_sample_loop(mf, torch.from_numpy(g["x_T"]), s, lambda step, x: noise[T - 1 - step])
+    return x0, torch.from_numpy(g["x0"])
+
+
+def test_tiny_ddpm_trajectory():
+    x0, ref = _traj(ARCH_TINY, synthetic_state_dict(ARCH_TINY, 0), "tiny_ddpm_traj", 0.02)
+    np.testing.assert_allclose(x0.numpy(), ref.numpy(), atol=1e-4, rtol=0)
+
+
+def test_tiny_cfg_trajectory():
+    g = golden("tiny_cfg_traj")
+    x0, ref = _traj(ARCH_TINY_CFG, synthetic_state_dict(ARCH_TINY_CFG, 0), "tiny_cfg_traj", 0.028,
+                    labels=torch.from_numpy(g["labels"]), w=float(g["w"]))
+    np.testing.assert_allclose(x0.numpy(), ref.numpy(), atol=1e-4, rtol=0)
+
+
+def test_verifiers():
+    g = golden("verifiers")
+    for case in ("b1_neg", "b4_neg", "b4_pos", "b2_neg"):
+        im = torch.from_numpy(g[case + "_images"])
+        for kind, fn in R.VERIFIERS.items():
+            want = float(g[f"{case}_{kind}"])
+            got = fn(im)
+            if math.isnan(want):
+                assert math.isnan(got)
+            else:
+                assert abs(got - want) <= 1e-6, (case, kind, got, want)
+
+
+def test_search_outcomes_T5():
+    g = golden("search_T5")
+    sd = synthetic_state_dict(ARCH_TINY, 0)
+    s = R.schedule(1e-4, 0.02, 5)
+    f = _fw(ARCH_TINY, sd)
+
+    def denoise(noise):
+        return R.p_sample_loop(f, noise, s, lambda step, x: torch.randn_like(x))
+
+    torch.manual_seed(0)
+    bn, bs, scores = R.random_search(4, (1, 3, 32, 32), denoise, R.oracle_score)
+    np.testing.assert_allclose(scores, g["random_scores"], atol=1e-6)
+    np.testing.assert_array_equal(bn.numpy(), g["random_best_noise"])
+    torch.manual_seed(1)
+    init = torch.randn(1, 3, 32, 32)
+    bn, bs, h = R.zero_order_search(init, 3, 0.95, 2, denoise, R.oracle_score)
+    np.testing.assert_allclose(np.array(h["scores"]), g["zo_scores"], atol=1e-6)
+    np.testing.assert_allclose(bn.numpy(), g["zo_best_noise"], atol=1e-6)
+    torch.manual_seed(2)
+    init = torch.randn(1, 3, 32, 32)
+    bn, bs, h = R.path_search(init, 3, 400, 0.1, denoise, R.oracle_score)
+    np.testing.assert_allclose(np.array(h["scores"]), g["path_scores"], atol=1e-6)
+    np.testing.assert_allclose(bn.numpy(), g["path_best_noise"], atol=1e-6)
