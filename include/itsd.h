@@ -1,0 +1,130 @@
+/*
+ * itsd.h — C ABI of libitsd_hip.so, the MI355X (gfx950) search-over-noise sampler.
+ *
+ * The reference exposes this path as Python duck-typed objects;
+ * each entry point below replaces one of them:
+ *
+ *   itsd_unet_create / _destroy  <- UNet(T, ch, ch_mult, attn, num_res_blocks, dropout)
+ *                                   + load_state_dict   (Diffusion/Model.py:213,
+ *                                   DiffusionFreeGuidence/ModelCondition.py:165,
+ *                                   Diffusion/Train.py:814-818)
+ *   itsd_unet_forward            <- UNet.forward(x, t[, labels])   (Model.py:265,
+ *                                   ModelCondition.py:206)
+ *   itsd_set_schedule            <- GaussianDiffusionSampler.__init__ tables
+ *                                   (Diffusion/Diffusion.py:51-65, DiffusionCondition.py:57-73)
+ *   itsd_sampler_run             <- GaussianDiffusionSampler.forward loop
+ *                                   (Diffusion.py:84-102, DiffusionCondition.py:89-105)
+ *   itsd_verify                  <- OracleVerifier / SelfSupervisedVerifier /
+ *                                   AestheticPredictor .score (search/verifier.py:45-66,
+ *                                   223-248, 262-287), batched per candidate
+ *   itsd_profile_forward         <- (no reference counterpart) per-kernel census used
+ *                                   by bench.py for the roofline line
+ *
+ * Conventions
+ *  - Every tensor argument is a DEVICE pointer owned by the caller; the library
+ *    borrows it for the stream-ordered duration of the call. Weights passed to
+ *    itsd_unet_create are HOST fp32 pointers (a state_dict on CPU); they are
+ *    repacked and copied, and may be freed after the call returns.
+ *  - Layouts at the boundary are the reference's: images NCHW fp32, timesteps and
+ *    labels int32 per sample. Internally activations are NHWC (bf16 or fp32).
+ *  - Every function returns ITSD_OK (0) or an error code; no exception or abort
+ *    crosses the ABI. itsd_last_error() returns a thread-local message.
+ *  - Calls are asynchronous on the given stream (a hipStream_t passed as void*;
+ *    NULL = the default stream) unless documented otherwise. One handle per
+ *    device/process; a handle is not thread-safe.
+ */
+#ifndef ITSD_H
+#define ITSD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ITSD_OK 0
+#define ITSD_ERR_INVALID 1   /* bad argument / shape / unsupported configuration */
+#define ITSD_ERR_HIP 2       /* a HIP runtime call failed */
+#define ITSD_ERR_WEIGHTS 3   /* state_dict key or shape mismatch (load_state_dict strict) */
+#define ITSD_ERR_NAN 4       /* the sampler produced a NaN (Diffusion.py:100 assert) */
+#define ITSD_ERR_OOM 5
+
+enum { ITSD_ARCH_DDPM = 0, ITSD_ARCH_CFG = 1 };
+enum { ITSD_PREC_FP32 = 0, ITSD_PREC_BF16 = 1 };
+enum { ITSD_VERIFY_ORACLE = 0, ITSD_VERIFY_SELFSUP = 1, ITSD_VERIFY_AESTHETIC = 2 };
+
+/* itsd_sampler_run flags */
+#define ITSD_RUN_GRAPH 1u   /* capture one denoising step in a hipGraph and replay it */
+#define ITSD_RUN_CLIP 2u    /* clip(x, -1, 1) after the last step (Diffusion.py:102) */
+#define ITSD_RUN_SYNC 4u    /* synchronise at the end and report ITSD_ERR_NAN */
+
+typedef struct itsd_unet itsd_unet;
+
+/* Constructor arguments of the reference UNets plus sizing. */
+typedef struct {
+  int32_t arch;            /* ITSD_ARCH_DDPM (Model.py) or ITSD_ARCH_CFG (ModelCondition.py) */
+  int32_t T;               /* model T (CFG: rows of the time-embedding table) */
+  int32_t ch;              /* 'channel' */
+  int32_t n_mult;
+  int32_t ch_mult[8];      /* 'channel_mult' */
+  int32_t n_attn;
+  int32_t attn[8];         /* 'attn' level indices (DDPM only) */
+  int32_t num_res_blocks;
+  int32_t img_size;        /* H = W */
+  int32_t num_labels;      /* CFG only */
+  int32_t max_batch;       /* largest n passed to forward/sampler (CFG: per-branch n) */
+  int32_t precision;       /* ITSD_PREC_FP32 (parity) or ITSD_PREC_BF16 (throughput) */
+} itsd_unet_desc;
+
+/* One state_dict entry (host fp32, contiguous, reference key name). */
+typedef struct {
+  const char* name;
+  const float* data;
+  int64_t numel;
+} itsd_tensor_view;
+
+int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights, int n_weights,
+                     int device, itsd_unet** out);
+int itsd_unet_destroy(itsd_unet* u);
+
+/* eps[n,3,H,W] = UNet(x[n,3,H,W], t[n]) (DDPM) or UNet(x, t, labels[n]) (CFG). */
+int itsd_unet_forward(itsd_unet* u, const float* x, const int32_t* t, const int32_t* labels,
+                      float* eps, int n, void* stream);
+
+/* Host fp32 tables of length T: coeff1, coeff2 and sqrt(var) (the fp32 casts the
+ * reference's extract() produces, Diffusion.py:9-16), plus the CFG weight w. */
+int itsd_set_schedule(itsd_unet* u, int T, const float* coeff1, const float* coeff2,
+                      const float* sqrt_var, float w);
+
+/* Run steps t_begin..t_end (inclusive, descending) of the ancestral sampler in
+ * place on x[n,3,H,W]. noise == NULL: z ~ N(0,1) from counter-based Philox keyed
+ * (seed, step, noise_offset + element); otherwise noise is [T][n][3][H][W] fp32 and
+ * step t uses noise[t] (t >= 1; the reference draws no noise at t = 0). labels: CFG only. */
+int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t_begin, int t_end,
+                     uint64_t seed, int64_t noise_offset, const float* noise, uint32_t flags, void* stream);
+
+/* out[c][e] = (pivot ? pivot[e] : 0) + scale * z, z ~ N(0,1) from Philox keyed
+ * (seed, stream_id, (cand_offset + c) * per_cand + e), for c < n_cand, e < per_cand.
+ * Candidate noises are thus a function of their GLOBAL index, so every rank can
+ * regenerate any candidate (search_algorithm.py:67 randn, :225 pivot + randn*(1-lambda)). */
+int itsd_noise(float* out, const float* pivot, int n_cand, int64_t per_cand, float scale, uint64_t seed,
+               uint32_t stream_id, int64_t cand_offset, void* stream);
+
+/* scores[c] = verifier(images[c*b:(c+1)*b]) for c < n_cand; images NCHW fp32. */
+int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w,
+                double* scores, void* stream);
+
+/* Census of one forward at batch n (synchronous): runs the op program eagerly with
+ * HIP events around every launch. Outputs (any may be NULL):
+ *   conv_ms / conv_flops / conv_launches : the implicit-GEMM conv kernel
+ *   total_ms                              : the whole forward (sum of launches) */
+int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, double* conv_ms,
+                         double* conv_flops, int* conv_launches, double* total_ms, void* stream);
+
+const char* itsd_last_error(void);
+int itsd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ITSD_H */

@@ -1,0 +1,852 @@
+// libitsd_hip runtime: the C ABI of include/itsd.h.
+//
+// Builds the UNet op program natively from the reference constructor arguments
+// (Diffusion/Model.py:212-262, DiffusionFreeGuidence/ModelCondition.py:164-203),
+// repacks the state_dict into MFMA-friendly layouts, owns one activation arena
+// sized for max_batch (288 GB of HBM makes a dedicated buffer per op affordable),
+// and drives the ancestral sampler loop (Diffusion.py:84-102) as one hipGraph
+// replayed T times; the timestep lives in device memory so the graph is
+// step-invariant and no host sync happens inside the loop.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+#include "itsd.h"
+
+namespace itsd {
+template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
+template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
+template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
+template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
+template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
+hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
+hipError_t launch_linear(const float*, int, int, const float*, const float*, int, int, float*, hipStream_t);
+hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hipStream_t);
+hipError_t launch_set_int(int*, int, hipStream_t);
+hipError_t launch_add_int(int*, int, hipStream_t);
+hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
+                        hipStream_t);
+}  // namespace itsd
+
+using namespace itsd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                           \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) return fail(ITSD_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define CHK(x)                  \
+  do {                          \
+    int r_ = (x);               \
+    if (r_ != ITSD_OK) return r_; \
+  } while (0)
+
+uint16_t host_f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// NHWC activation buffer (capacity = max batch), located at ws + off.
+struct Act {
+  size_t off;
+  int H, W, C;
+};
+
+enum OpKind { OP_GN, OP_CONV, OP_ATTN };
+
+struct Op {
+  OpKind kind;
+  int src1 = -1, src2 = -1, dst = -1;
+  // GN
+  size_t gamma = 0, beta = 0;  // fp32 offsets in the weight arena
+  int silu = 0;
+  // CONV
+  int ksize = 3, stride = 1, pad = 1, upsample = 0, zins = 0;
+  size_t wt = 0, bias = 0;
+  int Cout = 0, K = 0;
+  int temb_col = -1;
+  int resid = -1;
+  // ATTN
+  int S = 0, C = 0;
+};
+
+// Host staging for the weight arena: fp32 params and packed conv weights.
+struct Arena {
+  std::vector<char> host;
+  size_t add(const void* p, size_t bytes) {
+    size_t off = (host.size() + 255) & ~(size_t)255;
+    host.resize(off + bytes);
+    if (p) std::memcpy(host.data() + off, p, bytes);
+    return off;
+  }
+};
+
+struct GraphEntry {
+  std::tuple<int, const float*, const int32_t*, const float*, unsigned long long, int, long long> key;
+  hipGraphExec_t exec = nullptr;
+};
+
+}  // namespace
+
+struct itsd_unet {
+  itsd_unet_desc d{};
+  int device = 0;
+  bool bf16 = false;
+  size_t esz = 4;
+  bool cfg = false;
+  int H = 32, ch = 128, tdim = 512, sumC = 0;
+  int nb_max = 0;  // capacity in images (CFG: 2 * max_batch)
+
+  char* wdev = nullptr;
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  std::vector<Act> acts;
+  std::vector<Op> ops;
+  int head_out = -1, tail_g = -1, tail_in = -1;
+  size_t tail_gn_g = 0, tail_gn_b = 0;
+
+  // fp32 params (arena offsets)
+  size_t head_w = 0, head_b = 0, tail_w = 0, tail_b = 0;
+  size_t freq = 0, ttable = 0, W0t = 0, b0 = 0, W2t = 0, b2 = 0, Wpt = 0, bp = 0;
+  size_t ctable = 0, C1t = 0, cb1 = 0, C3t = 0, cb3 = 0, Wct = 0, bc = 0;
+
+  // scratch (separate allocation)
+  float* emb_buf = nullptr;   // [rows][ch]
+  float* h1_buf = nullptr;    // [rows][tdim]
+  float* te_buf = nullptr;    // [rows][tdim]
+  float* proj_buf = nullptr;  // [max_batch][sumC]
+  int rows_cap = 0;
+  float* cemb_table = nullptr;  // [num_labels+1][sumC] (CFG)
+  // sampler
+  int T_sched = 0;
+  float* coeff1 = nullptr;
+  float* coeff2 = nullptr;
+  float* sqrt_var = nullptr;
+  float* temb_table = nullptr;  // [T_sched][sumC]
+  float guide_w = 0.f, guide_w1 = 1.f;
+  int* d_t = nullptr;
+  int* d_nan = nullptr;
+
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::vector<GraphEntry> graphs;
+
+  template <typename P = float>
+  P* wp(size_t off) const { return (P*)(wdev + off); }
+  void* ap(int id) const { return ws + acts[id].off; }
+};
+
+namespace {
+
+struct Builder {
+  itsd_unet* u;
+  Arena ar;
+  std::unordered_map<std::string, std::pair<const float*, int64_t>> w;
+  size_t used = 0;
+  size_t ws_off = 0;
+  std::string err;
+  std::vector<std::pair<std::string, size_t>> temb_cols;  // resblock prefix -> column
+
+  const float* get(const std::string& name, int64_t numel) {
+    auto it = w.find(name);
+    if (it == w.end()) {
+      if (err.empty()) err = "missing key in state_dict: " + name;
+      return nullptr;
+    }
+    if (it->second.second != numel) {
+      if (err.empty())
+        err = "size mismatch for " + name + ": got " + std::to_string(it->second.second) + " elements, expected " +
+              std::to_string(numel);
+      return nullptr;
+    }
+    ++used;
+    return it->second.first;
+  }
+  size_t f32(const std::string& name, int64_t numel) {
+    const float* p = get(name, numel);
+    return ar.add(p, numel * 4);
+  }
+  int act(int H, int W, int C) {
+    Act a{ws_off, H, W, C};
+    size_t bytes = (size_t)u->nb_max * H * W * C * u->esz;
+    ws_off = (ws_off + bytes + 255) & ~(size_t)255;
+    u->acts.push_back(a);
+    return (int)u->acts.size() - 1;
+  }
+  // Packs conv weight(s) [Cout][Cin][k][k] into [Cout][K] with k = (ky*ks+kx)*Cin + ci.
+  // flip_t: source is ConvTranspose2d [Cin][Cout][k][k]; use the flipped kernel.
+  size_t pack(const std::vector<const float*>& parts, int Cpart, int Cin, int ks, bool flip_t = false) {
+    const int Cout = Cpart * (int)parts.size();
+    const int K = ks * ks * Cin;
+    std::vector<float> tmp((size_t)Cout * K, 0.f);
+    for (size_t pi = 0; pi < parts.size(); ++pi) {
+      const float* src = parts[pi];
+      if (!src) continue;
+      for (int co = 0; co < Cpart; ++co)
+        for (int ci = 0; ci < Cin; ++ci)
+          for (int ky = 0; ky < ks; ++ky)
+            for (int kx = 0; kx < ks; ++kx) {
+              float v;
+              if (!flip_t) v = src[(((size_t)co * Cin + ci) * ks + ky) * ks + kx];
+              else v = src[(((size_t)ci * Cpart + co) * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)];
+              tmp[((size_t)pi * Cpart + co) * K + (ky * ks + kx) * Cin + ci] = v;
+            }
+    }
+    if (u->bf16) {
+      std::vector<uint16_t> b(tmp.size());
+      for (size_t i = 0; i < tmp.size(); ++i) b[i] = host_f2bf(tmp[i]);
+      return ar.add(b.data(), b.size() * 2);
+    }
+    return ar.add(tmp.data(), tmp.size() * 4);
+  }
+  size_t concat_f32(const std::vector<const float*>& parts, int n) {
+    std::vector<float> tmp((size_t)n * parts.size(), 0.f);
+    for (size_t i = 0; i < parts.size(); ++i)
+      if (parts[i]) std::memcpy(tmp.data() + i * n, parts[i], n * 4);
+    return ar.add(tmp.data(), tmp.size() * 4);
+  }
+  // W [out][in] -> W^T [in][out] fp32
+  size_t transposed(const float* W, int out, int in) {
+    std::vector<float> tmp((size_t)out * in, 0.f);
+    if (W)
+      for (int o = 0; o < out; ++o)
+        for (int i = 0; i < in; ++i) tmp[(size_t)i * out + o] = W[(size_t)o * in + i];
+    return ar.add(tmp.data(), tmp.size() * 4);
+  }
+
+  void gn(int s1, int s2, int dst, const std::string& p, int C, int silu) {
+    Op o;
+    o.kind = OP_GN;
+    o.src1 = s1; o.src2 = s2; o.dst = dst;
+    o.gamma = f32(p + ".weight", C);
+    o.beta = f32(p + ".bias", C);
+    o.silu = silu;
+    u->ops.push_back(o);
+  }
+  void conv(int s1, int s2, int dst, size_t wt, size_t bias, int Cout, int ks, int stride, int pad, int ups,
+            int temb_col = -1, int resid = -1, int zins = 0) {
+    Op o;
+    o.kind = OP_CONV;
+    o.src1 = s1; o.src2 = s2; o.dst = dst;
+    o.wt = wt; o.bias = bias; o.Cout = Cout;
+    const int Cin = u->acts[s1].C + (s2 >= 0 ? u->acts[s2].C : 0);
+    o.K = ks * ks * Cin;
+    o.ksize = ks; o.stride = stride; o.pad = pad; o.upsample = ups; o.zins = zins;
+    o.temb_col = temb_col; o.resid = resid;
+    u->ops.push_back(o);
+  }
+  int conv_layer(int s1, int s2, const std::string& name, int Cout, int ks, int stride, int pad, int ups, int Hout,
+                 int Wout, int temb_col = -1, int resid = -1) {
+    const int Cin = u->acts[s1].C + (s2 >= 0 ? u->acts[s2].C : 0);
+    const float* W = get(name + ".weight", (int64_t)Cout * Cin * ks * ks);
+    size_t wt = pack({W}, Cout, Cin, ks);
+    size_t b = f32(name + ".bias", Cout);
+    int dst = act(Hout, Wout, Cout);
+    conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
+    return dst;
+  }
+
+  int resblock(int x1, int x2, const std::string& p, int in_ch, int out_ch, bool attn) {
+    const int H = u->acts[x1].H, W = u->acts[x1].W;
+    const int col = u->sumC;
+    u->sumC += out_ch;
+    temb_cols.push_back({p, (size_t)col});
+    int g1 = act(H, W, in_ch);
+    gn(x1, x2, g1, p + ".block1.0", in_ch, 1);
+    int h1 = conv_layer(g1, -1, p + ".block1.2", out_ch, 3, 1, 1, 0, H, W, col);
+    int g2 = act(H, W, out_ch);
+    gn(h1, -1, g2, p + ".block2.0", out_ch, 1);
+    int resid = x1;
+    if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
+    int o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
+    if (attn) {
+      const std::string a = p + ".attn";
+      int ga = act(H, W, out_ch);
+      gn(o, -1, ga, a + ".group_norm", out_ch, 0);
+      const int64_t cc = (int64_t)out_ch * out_ch;
+      size_t wqkv = pack({get(a + ".proj_q.weight", cc), get(a + ".proj_k.weight", cc), get(a + ".proj_v.weight", cc)},
+                         out_ch, out_ch, 1);
+      size_t bqkv = concat_f32({get(a + ".proj_q.bias", out_ch), get(a + ".proj_k.bias", out_ch),
+                                get(a + ".proj_v.bias", out_ch)}, out_ch);
+      int qkv = act(H, W, 3 * out_ch);
+      conv(ga, -1, qkv, wqkv, bqkv, 3 * out_ch, 1, 1, 0, 0);
+      int ao = act(H, W, out_ch);
+      Op at;
+      at.kind = OP_ATTN;
+      at.src1 = qkv; at.dst = ao; at.S = H * W; at.C = out_ch;
+      u->ops.push_back(at);
+      o = conv_layer(ao, -1, a + ".proj", out_ch, 1, 1, 0, 0, H, W, -1, o);
+    }
+    return o;
+  }
+};
+
+int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
+  Builder b;
+  b.u = u;
+  for (int i = 0; i < nviews; ++i) b.w[views[i].name] = {views[i].data, views[i].numel};
+  const itsd_unet_desc& d = u->d;
+  const int ch = d.ch, tdim = 4 * ch, H = d.img_size;
+  u->ch = ch; u->tdim = tdim; u->H = H;
+
+  // embeddings
+  if (!u->cfg) {
+    u->freq = b.f32("time_embedding.freq_coeffs", ch / 2);
+    u->W0t = b.transposed(b.get("time_embedding.timembedding.0.weight", (int64_t)tdim * ch), tdim, ch);
+    u->b0 = b.f32("time_embedding.timembedding.0.bias", tdim);
+    u->W2t = b.transposed(b.get("time_embedding.timembedding.2.weight", (int64_t)tdim * tdim), tdim, tdim);
+    u->b2 = b.f32("time_embedding.timembedding.2.bias", tdim);
+  } else {
+    u->ttable = b.f32("time_embedding.timembedding.0.weight", (int64_t)d.T * ch);
+    u->W0t = b.transposed(b.get("time_embedding.timembedding.1.weight", (int64_t)tdim * ch), tdim, ch);
+    u->b0 = b.f32("time_embedding.timembedding.1.bias", tdim);
+    u->W2t = b.transposed(b.get("time_embedding.timembedding.3.weight", (int64_t)tdim * tdim), tdim, tdim);
+    u->b2 = b.f32("time_embedding.timembedding.3.bias", tdim);
+    u->ctable = b.f32("cond_embedding.condEmbedding.0.weight", (int64_t)(d.num_labels + 1) * ch);
+    u->C1t = b.transposed(b.get("cond_embedding.condEmbedding.1.weight", (int64_t)tdim * ch), tdim, ch);
+    u->cb1 = b.f32("cond_embedding.condEmbedding.1.bias", tdim);
+    u->C3t = b.transposed(b.get("cond_embedding.condEmbedding.3.weight", (int64_t)tdim * tdim), tdim, tdim);
+    u->cb3 = b.f32("cond_embedding.condEmbedding.3.bias", tdim);
+  }
+  u->head_w = b.f32("head.weight", (int64_t)ch * 27);
+  u->head_b = b.f32("head.bias", ch);
+  u->head_out = b.act(H, H, ch);
+
+  std::vector<int> hs{u->head_out};
+  int cur = u->head_out;
+  int now = ch;
+  int ndown = 0;
+  auto P = [](const char* s, int i) { return std::string(s) + "." + std::to_string(i); };
+  for (int i = 0; i < d.n_mult; ++i) {
+    const int out = ch * d.ch_mult[i];
+    bool at = false;
+    for (int k = 0; k < d.n_attn; ++k) at |= (d.attn[k] == i);
+    if (u->cfg) at = true;
+    for (int r = 0; r < d.num_res_blocks; ++r) {
+      cur = b.resblock(cur, -1, P("downblocks", ndown++), now, out, at);
+      now = out;
+      hs.push_back(cur);
+    }
+    if (i != d.n_mult - 1) {
+      const std::string p = P("downblocks", ndown++);
+      const int Hc = b.u->acts[cur].H;
+      if (!u->cfg) {
+        cur = b.conv_layer(cur, -1, p + ".main", now, 3, 2, 1, 0, Hc / 2, Hc / 2);
+      } else {  // c1(x) + c2(x), ModelCondition.py:71-73
+        int t1 = b.conv_layer(cur, -1, p + ".c1", now, 3, 2, 1, 0, Hc / 2, Hc / 2);
+        cur = b.conv_layer(cur, -1, p + ".c2", now, 5, 2, 2, 0, Hc / 2, Hc / 2, -1, t1);
+      }
+      hs.push_back(cur);
+    }
+  }
+  cur = b.resblock(cur, -1, "middleblocks.0", now, now, true);
+  cur = b.resblock(cur, -1, "middleblocks.1", now, now, false);
+  int nup = 0;
+  for (int i = d.n_mult - 1; i >= 0; --i) {
+    const int out = ch * d.ch_mult[i];
+    bool at = false;
+    for (int k = 0; k < d.n_attn; ++k) at |= (d.attn[k] == i);
+    if (u->cfg) at = false;
+    for (int r = 0; r < d.num_res_blocks + 1; ++r) {
+      int skip = hs.back();
+      hs.pop_back();
+      cur = b.resblock(cur, skip, P("upblocks", nup++), now + u->acts[skip].C, out, at);
+      now = out;
+    }
+    if (i != 0) {
+      const std::string p = P("upblocks", nup++);
+      const int Hc = b.u->acts[cur].H;
+      if (!u->cfg) {
+        cur = b.conv_layer(cur, -1, p + ".main", now, 3, 1, 1, 1, 2 * Hc, 2 * Hc);
+      } else {  // ConvTranspose2d(5, 2, 2, 1) then Conv 3x3, ModelCondition.py:83-85
+        const float* Wt = b.get(p + ".t.weight", (int64_t)now * now * 25);
+        size_t wt = b.pack({Wt}, now, now, 5, true);
+        size_t bt = b.f32(p + ".t.bias", now);
+        int tmp = b.act(2 * Hc, 2 * Hc, now);
+        b.conv(cur, -1, tmp, wt, bt, now, 5, 1, 2, 0, -1, -1, 1);
+        cur = b.conv_layer(tmp, -1, p + ".c", now, 3, 1, 1, 0, 2 * Hc, 2 * Hc);
+      }
+    }
+  }
+  if (!hs.empty()) return fail(ITSD_ERR_INVALID, "internal: skip stack not empty");
+  u->tail_in = cur;
+  u->tail_gn_g = b.f32("tail.0.weight", now);
+  u->tail_gn_b = b.f32("tail.0.bias", now);
+  u->tail_g = b.act(H, H, now);
+  u->tail_w = b.f32("tail.2.weight", (int64_t)3 * now * 9);
+  u->tail_b = b.f32("tail.2.bias", 3);
+
+  // all ResBlock temb_proj (and cond_proj) Linears as one [tdim][sumC] matrix
+  {
+    std::vector<float> Wp((size_t)u->sumC * tdim), bpv(u->sumC), Wc, bcv;
+    if (u->cfg) { Wc.resize(Wp.size()); bcv.resize(u->sumC); }
+    for (size_t k = 0; k < b.temb_cols.size(); ++k) {
+      const std::string& p = b.temb_cols[k].first;
+      const size_t col = b.temb_cols[k].second;
+      const size_t next = (k + 1 < b.temb_cols.size()) ? b.temb_cols[k + 1].second : (size_t)u->sumC;
+      const int oc = (int)(next - col);
+      auto fill = [&](const std::string& nm, std::vector<float>& Wd, std::vector<float>& bd) {
+        const float* W = b.get(nm + ".weight", (int64_t)oc * tdim);
+        const float* bb = b.get(nm + ".bias", oc);
+        if (!W || !bb) return;
+        for (int o = 0; o < oc; ++o) {
+          for (int i = 0; i < tdim; ++i) Wd[(size_t)i * u->sumC + col + o] = W[(size_t)o * tdim + i];
+          bd[col + o] = bb[o];
+        }
+      };
+      fill(p + ".temb_proj.1", Wp, bpv);
+      if (u->cfg) fill(p + ".cond_proj.1", Wc, bcv);
+    }
+    u->Wpt = b.ar.add(Wp.data(), Wp.size() * 4);
+    u->bp = b.ar.add(bpv.data(), bpv.size() * 4);
+    if (u->cfg) {
+      u->Wct = b.ar.add(Wc.data(), Wc.size() * 4);
+      u->bc = b.ar.add(bcv.data(), bcv.size() * 4);
+    }
+  }
+  if (!b.err.empty()) return fail(ITSD_ERR_WEIGHTS, b.err);
+  if ((int)b.used != nviews) {
+    return fail(ITSD_ERR_WEIGHTS, "state_dict has " + std::to_string(nviews) + " entries, model uses " +
+                                      std::to_string(b.used) + " (unexpected keys present)");
+  }
+  // device arenas
+  HIPCHK(hipMalloc(&u->wdev, b.ar.host.size()));
+  HIPCHK(hipMemcpy(u->wdev, b.ar.host.data(), b.ar.host.size(), hipMemcpyHostToDevice));
+  u->ws_bytes = b.ws_off;
+  HIPCHK(hipMalloc(&u->ws, u->ws_bytes));
+  return ITSD_OK;
+}
+
+// ------------------------------------------------------------------------- program execution
+struct RunCtx {
+  int nb;                // images in the UNet batch
+  const float* x;        // head input NCHW
+  int x_mod;             // head reads x[img % x_mod]
+  const float* temb;     // temb rows/table base
+  const int* tsel;       // device t (table mode) or null
+  long long temb_img_stride;
+  const int32_t* labels; // CFG labels
+  int label_mod;
+  int uncond_from;
+  TailArgs tail;
+  // census
+  bool census = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>>* evs = nullptr;
+  std::vector<int>* ev_kind = nullptr;
+  std::vector<double>* ev_flops = nullptr;
+};
+
+int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (o.kind == OP_GN) {
+    GNArgs a{};
+    a.src1 = u->ap(o.src1);
+    a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
+    a.C1 = u->acts[o.src1].C;
+    a.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
+    a.HW = u->acts[o.src1].H * u->acts[o.src1].W;
+    a.gamma = u->wp(o.gamma);
+    a.beta = u->wp(o.beta);
+    a.eps = 1e-5f;
+    a.silu = o.silu;
+    a.dst = u->ap(o.dst);
+    e = u->bf16 ? launch_groupnorm<bf16_t>(a, c.nb, s) : launch_groupnorm<float>(a, c.nb, s);
+  } else if (o.kind == OP_CONV) {
+    ConvArgs a{};
+    const Act& in = u->acts[o.src1];
+    const Act& out = u->acts[o.dst];
+    a.src1 = u->ap(o.src1);
+    a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
+    a.C1 = in.C;
+    a.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
+    a.Hin = in.H; a.Win = in.W; a.Hout = out.H; a.Wout = out.W;
+    a.ksize = o.ksize; a.stride = o.stride; a.pad = o.pad; a.upsample = o.upsample;
+    a.wt = u->wdev + o.wt;
+    a.Cout = o.Cout; a.K = o.K;
+    a.bias = u->wp(o.bias);
+    if (o.temb_col >= 0) {
+      a.temb = c.temb + o.temb_col;
+      a.temb_tsel = c.tsel;
+      a.temb_row_stride = u->sumC;
+      a.temb_img_stride = c.temb_img_stride;
+      if (u->cfg) {
+        a.cemb = u->cemb_table + o.temb_col;
+        a.cemb_labels = (const int*)c.labels;
+        a.cemb_row_stride = u->sumC;
+        a.cemb_label_mod = c.label_mod;
+        a.cemb_uncond_from = c.uncond_from;
+      }
+    }
+    a.resid = o.resid >= 0 ? u->ap(o.resid) : nullptr;
+    a.out = u->ap(o.dst);
+    a.M = c.nb * out.H * out.W;
+    a.zins = o.zins;
+    {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
+      const int epc = u->bf16 ? 8 : 4;
+      if (a.C1 % epc || a.C2 % epc || a.Cout % 4 || a.K % epc)
+        return fail(ITSD_ERR_INVALID, "conv channels must be multiples of " + std::to_string(epc));
+    }
+    e = u->bf16 ? launch_conv<bf16_t>(a, s) : launch_conv<float>(a, s);
+  } else {
+    AttnArgs a{};
+    a.qkv = u->ap(o.src1);
+    a.out = u->ap(o.dst);
+    a.S = o.S; a.C = o.C;
+    a.scale = (float)std::pow((double)o.C, -0.5);
+    e = u->bf16 ? launch_attn<bf16_t>(a, c.nb, s) : launch_attn<float>(a, c.nb, s);
+  }
+  if (e != hipSuccess) return fail(ITSD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+  return ITSD_OK;
+}
+
+double op_flops(const itsd_unet* u, const Op& o, int nb) {
+  if (o.kind == OP_CONV) {
+    const Act& out = u->acts[o.dst];
+    return 2.0 * nb * out.H * out.W * (double)o.Cout * o.K;
+  }
+  if (o.kind == OP_ATTN) return 2.0 * 2.0 * nb * (double)o.S * o.S * o.C;
+  return 0.0;
+}
+
+int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
+  auto mark = [&](int kind, double fl, const std::function<int()>& fn) -> int {
+    if (!c.census) return fn();
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, s));
+    int r = fn();
+    HIPCHK(hipEventRecord(b, s));
+    c.evs->push_back({a, b});
+    c.ev_kind->push_back(kind);
+    c.ev_flops->push_back(fl);
+    return r;
+  };
+  // head
+  CHK(mark(-1, 2.0 * c.nb * u->H * u->H * 27.0 * u->ch, [&]() -> int {
+    HeadArgs h{};
+    h.x = c.x;
+    h.w = u->wp(u->head_w);
+    h.b = u->wp(u->head_b);
+    h.out = u->ap(u->head_out);
+    h.H = u->H; h.W = u->H; h.Cout = u->ch; h.n = c.nb; h.x_img_mod = c.x_mod;
+    hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
+    return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
+  }));
+  for (const Op& o : u->ops) CHK(mark((int)o.kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
+  // tail GN + conv (+ sampler update)
+  Op g;
+  g.kind = OP_GN;
+  g.src1 = u->tail_in; g.dst = u->tail_g; g.gamma = u->tail_gn_g; g.beta = u->tail_gn_b; g.silu = 1;
+  CHK(mark(OP_GN, 0.0, [&]() { return launch_op(u, g, c, s); }));
+  CHK(mark(-2, 2.0 * c.tail.n * (c.tail.cfg ? 2 : 1) * u->H * u->H * 27.0 * u->acts[u->tail_in].C, [&]() -> int {
+    TailArgs t = c.tail;
+    t.g = u->ap(u->tail_g);
+    t.w = u->wp(u->tail_w);
+    t.b = u->wp(u->tail_b);
+    t.H = u->H; t.W = u->H; t.C = u->acts[u->tail_in].C;
+    hipError_t e = u->bf16 ? launch_tail<bf16_t>(t, s) : launch_tail<float>(t, s);
+    return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
+  }));
+  return ITSD_OK;
+}
+
+// temb rows: out[m][sumC] = Wp^T silu(MLP(emb(idx[m]))) + bp (Model.py:51-93 then each
+// ResBlock's temb_proj, :175-178); cond=true uses the label table / cond MLP.
+int temb_rows(itsd_unet* u, const int* idx, int M, int offset, bool cond, float* out, hipStream_t s) {
+  if (M > u->rows_cap) return fail(ITSD_ERR_INVALID, "temb rows exceed capacity");
+  const int ch = u->ch, td = u->tdim;
+  hipError_t e;
+  if (!cond) {
+    e = launch_emb_input(idx, M, u->cfg ? nullptr : u->wp(u->freq), u->cfg ? u->wp(u->ttable) : nullptr, ch,
+                         u->emb_buf, offset, s);
+  } else {
+    e = launch_emb_input(idx, M, nullptr, u->wp(u->ctable), ch, u->emb_buf, offset, s);
+  }
+  if (e != hipSuccess) return fail(ITSD_ERR_HIP, hipGetErrorString(e));
+  const float* W0 = u->wp(cond ? u->C1t : u->W0t);
+  const float* b0 = u->wp(cond ? u->cb1 : u->b0);
+  const float* W2 = u->wp(cond ? u->C3t : u->W2t);
+  const float* b2 = u->wp(cond ? u->cb3 : u->b2);
+  HIPCHK(launch_linear(u->emb_buf, M, ch, W0, b0, td, 0, u->h1_buf, s));
+  HIPCHK(launch_linear(u->h1_buf, M, td, W2, b2, td, 1, u->te_buf, s));
+  HIPCHK(launch_linear(u->te_buf, M, td, u->wp(cond ? u->Wct : u->Wpt), u->wp(cond ? u->bc : u->bp), u->sumC, 1,
+                       out, s));
+  return ITSD_OK;
+}
+
+int alloc_rows(itsd_unet* u, int rows) {
+  if (rows <= u->rows_cap) return ITSD_OK;
+  hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
+  HIPCHK(hipMalloc(&u->emb_buf, (size_t)rows * u->ch * 4));
+  HIPCHK(hipMalloc(&u->h1_buf, (size_t)rows * u->tdim * 4));
+  HIPCHK(hipMalloc(&u->te_buf, (size_t)rows * u->tdim * 4));
+  u->rows_cap = rows;
+  return ITSD_OK;
+}
+
+void clear_graphs(itsd_unet* u) {
+  for (auto& g : u->graphs)
+    if (g.exec) hipGraphExecDestroy(g.exec);
+  u->graphs.clear();
+}
+
+int check_batch(itsd_unet* u, int n) {
+  if (n <= 0 || n > u->d.max_batch)
+    return fail(ITSD_ERR_INVALID, "batch " + std::to_string(n) + " outside [1, max_batch=" +
+                                      std::to_string(u->d.max_batch) + "]");
+  return ITSD_OK;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int itsd_version(void) { return 1; }
+
+const char* itsd_last_error(void) { return g_err.c_str(); }
+
+int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights, int n_weights, int device,
+                     itsd_unet** out) {
+  if (!desc || !out || (!weights && n_weights)) return fail(ITSD_ERR_INVALID, "null argument");
+  const itsd_unet_desc& d = *desc;
+  if (d.arch != ITSD_ARCH_DDPM && d.arch != ITSD_ARCH_CFG) return fail(ITSD_ERR_INVALID, "unknown arch");
+  if (d.ch <= 0 || d.ch % 32 || d.n_mult < 1 || d.n_mult > 8 || d.n_attn < 0 || d.n_attn > 8 ||
+      d.num_res_blocks < 1 || d.max_batch < 1 || d.img_size < 8)
+    return fail(ITSD_ERR_INVALID, "invalid UNet descriptor");
+  if (d.img_size % (1 << (d.n_mult - 1))) return fail(ITSD_ERR_INVALID, "img_size not divisible by the down path");
+  for (int k = 0; k < d.n_attn; ++k)
+    if (d.attn[k] < 0 || d.attn[k] >= d.n_mult) return fail(ITSD_ERR_INVALID, "attn index out of bound");
+  if (d.precision != ITSD_PREC_FP32 && d.precision != ITSD_PREC_BF16) return fail(ITSD_ERR_INVALID, "precision");
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<itsd_unet> u(new itsd_unet());
+  u->d = d;
+  u->device = device;
+  u->bf16 = d.precision == ITSD_PREC_BF16;
+  u->esz = u->bf16 ? 2 : 4;
+  u->cfg = d.arch == ITSD_ARCH_CFG;
+  u->nb_max = d.max_batch * (u->cfg ? 2 : 1);
+  CHK(build(u.get(), weights, n_weights));
+  HIPCHK(hipStreamCreateWithFlags(&u->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&u->ev_in, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&u->ev_out, hipEventDisableTiming));
+  HIPCHK(hipMalloc(&u->d_t, 64));
+  HIPCHK(hipMalloc(&u->d_nan, 64));
+  HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
+  CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
+  if (u->cfg) {
+    HIPCHK(hipMalloc(&u->cemb_table, (size_t)(d.num_labels + 1) * u->sumC * 4));
+    CHK(temb_rows(u.get(), nullptr, d.num_labels + 1, 0, true, u->cemb_table, u->stream));
+    HIPCHK(hipStreamSynchronize(u->stream));
+  }
+  *out = u.release();
+  return ITSD_OK;
+}
+
+int itsd_unet_destroy(itsd_unet* u) {
+  if (!u) return ITSD_OK;
+  hipSetDevice(u->device);
+  clear_graphs(u);
+  hipFree(u->wdev); hipFree(u->ws); hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
+  hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
+  hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan);
+  if (u->stream) hipStreamDestroy(u->stream);
+  if (u->ev_in) hipEventDestroy(u->ev_in);
+  if (u->ev_out) hipEventDestroy(u->ev_out);
+  delete u;
+  return ITSD_OK;
+}
+
+int itsd_unet_forward(itsd_unet* u, const float* x, const int32_t* t, const int32_t* labels, float* eps, int n,
+                      void* stream) {
+  if (!u || !x || !t || !eps) return fail(ITSD_ERR_INVALID, "null argument");
+  if (u->cfg && !labels) return fail(ITSD_ERR_INVALID, "CFG UNet needs labels");
+  CHK(check_batch(u, n));
+  hipStream_t cs = (hipStream_t)stream;
+  hipStream_t s = u->stream;
+  HIPCHK(hipEventRecord(u->ev_in, cs));
+  HIPCHK(hipStreamWaitEvent(s, u->ev_in, 0));
+  CHK(temb_rows(u, t, n, 0, false, u->proj_buf, s));
+  RunCtx c{};
+  c.nb = n; c.x = x; c.x_mod = n;
+  c.temb = u->proj_buf; c.tsel = nullptr; c.temb_img_stride = u->sumC;
+  c.labels = labels; c.label_mod = n; c.uncond_from = -1;
+  c.tail.n = n; c.tail.cfg = 0; c.tail.step_mode = 0; c.tail.eps_out = eps;
+  CHK(run_program(u, c, s));
+  HIPCHK(hipEventRecord(u->ev_out, s));
+  HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
+  return ITSD_OK;
+}
+
+int itsd_set_schedule(itsd_unet* u, int T, const float* coeff1, const float* coeff2, const float* sqrt_var, float w) {
+  if (!u || T < 1 || !coeff1 || !coeff2 || !sqrt_var) return fail(ITSD_ERR_INVALID, "bad schedule");
+  if (u->cfg && T > u->d.T)
+    return fail(ITSD_ERR_INVALID, "CFG time-embedding table has " + std::to_string(u->d.T) + " rows < sampler T");
+  HIPCHK(hipSetDevice(u->device));
+  clear_graphs(u);
+  hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var); hipFree(u->temb_table);
+  u->coeff1 = u->coeff2 = u->sqrt_var = u->temb_table = nullptr;
+  HIPCHK(hipMalloc(&u->coeff1, T * 4));
+  HIPCHK(hipMalloc(&u->coeff2, T * 4));
+  HIPCHK(hipMalloc(&u->sqrt_var, T * 4));
+  HIPCHK(hipMemcpy(u->coeff1, coeff1, T * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(u->coeff2, coeff2, T * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(u->sqrt_var, sqrt_var, T * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&u->temb_table, (size_t)T * u->sumC * 4));
+  CHK(alloc_rows(u, T));
+  CHK(temb_rows(u, nullptr, T, 0, false, u->temb_table, u->stream));
+  HIPCHK(hipStreamSynchronize(u->stream));
+  u->T_sched = T;
+  u->guide_w = w;
+  u->guide_w1 = (float)(1.0 + (double)w);
+  return ITSD_OK;
+}
+
+int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t_begin, int t_end, uint64_t seed,
+                     int64_t noise_offset, const float* noise, uint32_t flags, void* stream) {
+  if (!u || !x) return fail(ITSD_ERR_INVALID, "null argument");
+  if (!u->T_sched) return fail(ITSD_ERR_INVALID, "itsd_set_schedule not called");
+  if (u->cfg && !labels) return fail(ITSD_ERR_INVALID, "CFG sampler needs labels");
+  CHK(check_batch(u, n));
+  if (t_begin >= u->T_sched || t_end < 0 || t_end > t_begin) return fail(ITSD_ERR_INVALID, "bad step range");
+  HIPCHK(hipSetDevice(u->device));
+  hipStream_t cs = (hipStream_t)stream;
+  hipStream_t s = u->stream;
+  HIPCHK(hipEventRecord(u->ev_in, cs));
+  HIPCHK(hipStreamWaitEvent(s, u->ev_in, 0));
+  const int clip_at = (flags & ITSD_RUN_CLIP) ? t_end : -1;
+
+  RunCtx c{};
+  c.nb = u->cfg ? 2 * n : n;
+  c.x = x; c.x_mod = n;
+  c.temb = u->temb_table; c.tsel = u->d_t; c.temb_img_stride = 0;
+  c.labels = labels; c.label_mod = n; c.uncond_from = u->cfg ? n : -1;
+  TailArgs& t = c.tail;
+  t.n = n; t.cfg = u->cfg ? 1 : 0; t.guide_w = u->guide_w; t.guide_w1 = u->guide_w1;
+  t.step_mode = 1; t.x = x; t.tsel = u->d_t;
+  t.coeff1 = u->coeff1; t.coeff2 = u->coeff2; t.sqrt_var = u->sqrt_var;
+  t.noise = noise; t.seed = seed; t.noise_offset = noise_offset; t.clip_at = clip_at; t.nan_flag = u->d_nan;
+
+  HIPCHK(hipMemsetAsync(u->d_nan, 0, 4, s));
+  HIPCHK(launch_set_int(u->d_t, t_begin, s));
+  const int steps = t_begin - t_end + 1;
+  if (flags & ITSD_RUN_GRAPH) {
+    auto key = std::make_tuple(n, (const float*)x, labels, noise, (unsigned long long)seed, clip_at, (long long)noise_offset);
+    hipGraphExec_t exec = nullptr;
+    for (auto& g : u->graphs)
+      if (g.key == key) exec = g.exec;
+    if (!exec) {
+      HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      int r = run_program(u, c, s);
+      if (r == ITSD_OK && launch_add_int(u->d_t, -1, s) != hipSuccess) r = fail(ITSD_ERR_HIP, "add_int");
+      hipGraph_t graph = nullptr;
+      hipError_t e = hipStreamEndCapture(s, &graph);
+      if (r != ITSD_OK) { if (graph) hipGraphDestroy(graph); return r; }
+      if (e != hipSuccess) return fail(ITSD_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
+      e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      hipGraphDestroy(graph);
+      if (e != hipSuccess) return fail(ITSD_ERR_HIP, std::string("instantiate: ") + hipGetErrorString(e));
+      if (u->graphs.size() >= 4) { hipGraphExecDestroy(u->graphs.front().exec); u->graphs.erase(u->graphs.begin()); }
+      u->graphs.push_back({key, exec});
+    }
+    for (int i = 0; i < steps; ++i) HIPCHK(hipGraphLaunch(exec, s));
+  } else {
+    for (int i = 0; i < steps; ++i) {
+      CHK(run_program(u, c, s));
+      HIPCHK(launch_add_int(u->d_t, -1, s));
+    }
+  }
+  HIPCHK(hipEventRecord(u->ev_out, s));
+  HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
+  if (flags & ITSD_RUN_SYNC) {
+    HIPCHK(hipStreamSynchronize(s));
+    int flag = 0;
+    HIPCHK(hipMemcpy(&flag, u->d_nan, 4, hipMemcpyDeviceToHost));
+    if (flag) return fail(ITSD_ERR_NAN, "nan in tensor.");
+  }
+  return ITSD_OK;
+}
+
+int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w, double* scores, void* stream) {
+  if (!images || !scores || n_cand < 1 || b < 1) return fail(ITSD_ERR_INVALID, "bad verify arguments");
+  if (kind < 0 || kind > 2) return fail(ITSD_ERR_INVALID, "unknown verifier kind");
+  if (kind == ITSD_VERIFY_SELFSUP && (c * 64 > 192 || h % 8 || w % 8 || b > 64))
+    return fail(ITSD_ERR_INVALID, "selfsup verifier needs c<=3, h,w divisible by 8, b<=64");
+  HIPCHK(launch_verify(kind, images, n_cand, b, c, h, w, scores, (hipStream_t)stream));
+  return ITSD_OK;
+}
+
+int itsd_noise(float* out, const float* pivot, int n_cand, int64_t per_cand, float scale, uint64_t seed,
+               uint32_t stream_id, int64_t cand_offset, void* stream) {
+  if (!out || n_cand < 0 || per_cand < 1) return fail(ITSD_ERR_INVALID, "bad noise arguments");
+  if (n_cand == 0) return ITSD_OK;
+  HIPCHK(launch_noise(out, pivot, n_cand, per_cand, scale, seed, stream_id, cand_offset, (hipStream_t)stream));
+  return ITSD_OK;
+}
+
+int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, double* conv_ms, double* conv_flops,
+                         int* conv_launches, double* total_ms, void* stream) {
+  if (!u || !x || !t) return fail(ITSD_ERR_INVALID, "null argument");
+  if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_forward: DDPM only");
+  CHK(check_batch(u, n));
+  HIPCHK(hipSetDevice(u->device));
+  hipStream_t s = u->stream;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  float* eps = nullptr;
+  HIPCHK(hipMalloc(&eps, (size_t)n * 3 * u->H * u->H * 4));
+  CHK(temb_rows(u, t, n, 0, false, u->proj_buf, s));
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+  std::vector<int> kinds;
+  std::vector<double> fl;
+  RunCtx c{};
+  c.nb = n; c.x = x; c.x_mod = n;
+  c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
+  c.label_mod = n; c.uncond_from = -1;
+  c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
+  c.census = true; c.evs = &evs; c.ev_kind = &kinds; c.ev_flops = &fl;
+  int r = run_program(u, c, s);
+  hipError_t e = hipStreamSynchronize(s);
+  double cm = 0, cf = 0, tm = 0;
+  int cl = 0;
+  for (size_t i = 0; i < evs.size(); ++i) {
+    float ms = 0.f;
+    if (r == ITSD_OK && e == hipSuccess) hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
+    tm += ms;
+    if (kinds[i] == OP_CONV) { cm += ms; cf += fl[i]; ++cl; }
+    hipEventDestroy(evs[i].first);
+    hipEventDestroy(evs[i].second);
+  }
+  hipFree(eps);
+  CHK(r);
+  HIPCHK(e);
+  if (conv_ms) *conv_ms = cm;
+  if (conv_flops) *conv_flops = cf;
+  if (conv_launches) *conv_launches = cl;
+  if (total_ms) *total_ms = tm;
+  return ITSD_OK;
+}
+
+}  // extern "C"

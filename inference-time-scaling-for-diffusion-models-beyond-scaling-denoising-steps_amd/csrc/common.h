@@ -1,0 +1,125 @@
+// Shared device helpers and kernel argument structs for libitsd_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace itsd {
+
+typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN stays NaN
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float load(const float* p) { return *p; }
+  static __device__ __forceinline__ float to(float v) { return v; }
+  static __device__ __forceinline__ float tof(float v) { return v; }
+};
+template <> struct Elem<bf16_t> {
+  static __device__ __forceinline__ float load(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ bf16_t to(float v) { return f2bf(v); }
+  static __device__ __forceinline__ float tof(bf16_t v) { return bf2f(v); }
+};
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Wave64 reductions.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ----------------------------------------------------------------------------- args
+// Implicit-GEMM convolution over NHWC activations (see conv.hip).
+struct ConvArgs {
+  const void* src1;  // [n][Hin][Win][C1]
+  const void* src2;  // [n][Hin][Win][C2] (channel-concat second source, Model.py:280) or null
+  int C1, C2;
+  int Hin, Win, Hout, Wout;
+  int ksize, stride, pad, upsample;  // upsample: nearest x2 folded into addressing (Model.py:123)
+  int zins;                          // zero-insertion (ConvTranspose2d s2 as a gather conv, ModelCondition.py:80)
+  const void* wt;                    // packed [Cout][K], K = ksize*ksize*(C1+C2), k=(ky*ks+kx)*Cin+ci
+  int Cout, K;
+  const float* bias;                 // [Cout]
+  // epilogue additive vectors (ResBlock temb_proj, Model.py:204; CFG cond_proj ModelCondition.py:156)
+  const float* temb;                 // temb[(tsel? *tsel*row : 0) + img*img_stride + co]
+  const int* temb_tsel;
+  long long temb_row_stride, temb_img_stride;
+  const float* cemb;                 // cemb[labels[img]*row + co]
+  const int* cemb_labels;
+  long long cemb_row_stride;
+  int cemb_label_mod;                // labels index = img % mod (CFG cond||uncond batch)
+  int cemb_uncond_from;              // images >= this use label 0 (uncond half); <0 disables
+  const void* resid;                 // [M][Cout] same layout as out, or null
+  void* out;                         // [M][Cout]
+  int M;                             // n * Hout * Wout
+};
+
+struct GNArgs {
+  const void* src1; const void* src2;  // NHWC, C1 (+ C2) channels
+  int C1, C2, HW;
+  const float* gamma; const float* beta;
+  float eps;
+  int silu;
+  void* dst;                           // NHWC, C1+C2 channels
+};
+
+struct AttnArgs {
+  const void* qkv;  // [n][S][3C]
+  void* out;        // [n][S][C]
+  int S, C;
+  float scale;
+};
+
+struct HeadArgs {
+  const float* x;       // NCHW fp32 [n][3][H][W]
+  const float* w;       // [Cout][3][3][3] fp32 (reference layout)
+  const float* b;
+  void* out;            // NHWC [n][H][W][Cout]
+  int H, W, Cout, n;
+  int x_img_mod;        // image i reads x[i % x_img_mod] (CFG cond||uncond batch)
+};
+
+struct TailArgs {
+  const void* g;        // NHWC [nb][H][W][C] : silu(gn(h))
+  const float* w;       // [3][C][3][3] fp32 (reference layout)
+  const float* b;       // [3]
+  int H, W, C, n;       // n = output images
+  int cfg;              // eps = (1+w) eps(img) - w eps(img+n)  (DiffusionCondition.py:85)
+  float guide_w;        // w (fp32 cast of the Python float)
+  float guide_w1;       // (1 + w) computed in double then cast, as the reference's scalar
+  // mode
+  int step_mode;        // 0: write eps NCHW; 1: sampler update of x in place
+  float* eps_out;       // NCHW [n][3][H][W]
+  float* x;             // NCHW [n][3][H][W]
+  const int* tsel;      // current step t (device)
+  const float* coeff1; const float* coeff2; const float* sqrt_var;
+  const float* noise;   // [T][n][3][H][W] or null
+  unsigned long long seed;
+  long long noise_offset;  // Philox element offset (global candidate index * per-candidate elements)
+  int clip_at;          // clip when t == clip_at (-1: never)
+  int* nan_flag;
+};
+
+}  // namespace itsd

@@ -1,0 +1,483 @@
+// Non-GEMM kernels of the UNet step (gfx950): GroupNorm(+SiLU) over (dual-source)
+// NHWC activations, single-head attention core, head conv, tail conv fused with
+// the ancestral-sampler update, timestep/label embedding MLPs, per-candidate
+// verifiers, and the counter-based Philox normal generator.
+#include <math.h>
+
+#include "common.h"
+
+namespace itsd {
+
+// ============================================================================ GroupNorm
+// nn.GroupNorm(32, C, eps=1e-5) (Model.py:132,171,180,253) with optional Swish, over
+// the channel concat of two NHWC sources (the up path's torch.cat, Model.py:280; a
+// group may straddle the two sources). One block per (group, image); two-pass
+// mean / biased variance in fp64, then y = x*a + b with a = rstd*gamma,
+// b = beta - mean*a written to a contiguous NHWC buffer of C1+C2 channels.
+template <typename T>
+__global__ __launch_bounds__(256) void groupnorm_kernel(GNArgs a) {
+  const int g = blockIdx.x, img = blockIdx.y;
+  const int C = a.C1 + a.C2;
+  const int gs = C / 32;
+  const int E = gs * a.HW;
+  const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
+  const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
+  T* dst = (T*)a.dst + (size_t)img * a.HW * C;
+  __shared__ double red[4];
+  __shared__ float stat[2];
+  auto ld = [&](int e, int& p, int& c) -> float {
+    p = e / gs;
+    c = g * gs + (e - p * gs);
+    return c < a.C1 ? Elem<T>::tof(s1[(size_t)p * a.C1 + c]) : Elem<T>::tof(s2[(size_t)p * a.C2 + (c - a.C1)]);
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double s = 0.0;
+  for (int e = tid; e < E; e += 256) { int p, c; s += (double)ld(e, p, c); }
+  s = wave_sum_d(s);
+  if (lane == 0) red[wid] = s;
+  __syncthreads();
+  const double mean = (red[0] + red[1] + red[2] + red[3]) / (double)E;
+  __syncthreads();
+  double q = 0.0;
+  for (int e = tid; e < E; e += 256) { int p, c; const double d = (double)ld(e, p, c) - mean; q += d * d; }
+  q = wave_sum_d(q);
+  if (lane == 0) red[wid] = q;
+  __syncthreads();
+  if (tid == 0) {
+    const double var = (red[0] + red[1] + red[2] + red[3]) / (double)E;
+    stat[0] = (float)mean;
+    stat[1] = (float)(1.0 / sqrt(var + (double)a.eps));
+  }
+  __syncthreads();
+  const float mf = stat[0], rstd = stat[1];
+  for (int e = tid; e < E; e += 256) {
+    int p, c;
+    const float x = ld(e, p, c);
+    const float sc = rstd * a.gamma[c];
+    float y = x * sc + (a.beta[c] - mf * sc);
+    if (a.silu) y = silu(y);
+    dst[(size_t)p * C + c] = Elem<T>::to(y);
+  }
+}
+
+template <typename T>
+hipError_t launch_groupnorm(const GNArgs& a, int n, hipStream_t s) {
+  hipLaunchKernelGGL(groupnorm_kernel<T>, dim3(32, n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+template hipError_t launch_groupnorm<float>(const GNArgs&, int, hipStream_t);
+template hipError_t launch_groupnorm<bf16_t>(const GNArgs&, int, hipStream_t);
+
+// ============================================================================ attention core
+// AttnBlock core (Model.py:152-161): w = softmax(q k^T * C^-0.5) ; h = w v, single head,
+// S = H*W tokens of width C. Input is the fused q|k|v projection [n][S][3C].
+// One block per (32-query chunk, image); the 32 x S score tile lives in LDS (S <= 256).
+__host__ __device__ inline int att_qc(int S) { int q = 8192 / S; return q < 1 ? 1 : (q > 32 ? 32 : q); }
+template <typename T>
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) float P[];  // [ATT_QC][S]
+  const int img = blockIdx.y, q0 = blockIdx.x * att_qc(a.S);
+  const int S = a.S, C = a.C, C3 = 3 * a.C;
+  const T* base = (const T*)a.qkv + (size_t)img * S * C3;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nq = min(att_qc(S), S - q0);
+  // scores
+  for (int idx = tid; idx < nq * S; idx += 256) {
+    const int r = idx / S, j = idx - r * S;
+    const T* qp = base + (size_t)(q0 + r) * C3;
+    const T* kp = base + (size_t)j * C3 + C;
+    float acc = 0.0f;
+    for (int c = 0; c < C; c += EPC) {
+      const u32x4 qv = *(const u32x4*)(qp + c);
+      const u32x4 kv = *(const u32x4*)(kp + c);
+      const T* qe = (const T*)&qv;
+      const T* ke = (const T*)&kv;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) acc = fmaf(Elem<T>::tof(qe[e]), Elem<T>::tof(ke[e]), acc);
+    }
+    P[r * S + j] = acc * a.scale;
+  }
+  __syncthreads();
+  // softmax rows (one wave per row)
+  for (int r = wid; r < nq; r += 4) {
+    float m = -INFINITY;
+    for (int j = lane; j < S; j += 64) m = fmaxf(m, P[r * S + j]);
+    m = wave_max(m);
+    float sum = 0.0f;
+    for (int j = lane; j < S; j += 64) { const float e = expf(P[r * S + j] - m); P[r * S + j] = e; sum += e; }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+    for (int j = lane; j < S; j += 64) P[r * S + j] *= inv;
+  }
+  __syncthreads();
+  // out = P v
+  T* out = (T*)a.out + (size_t)img * S * C;
+  for (int idx = tid; idx < nq * C; idx += 256) {
+    const int r = idx / C, c = idx - r * C;
+    const T* vp = base + 2 * C + c;
+    float acc = 0.0f;
+    for (int j = 0; j < S; ++j) acc = fmaf(P[r * S + j], Elem<T>::tof(vp[(size_t)j * C3]), acc);
+    out[(size_t)(q0 + r) * C + c] = Elem<T>::to(acc);
+  }
+}
+
+template <typename T>
+hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
+  const int qc = att_qc(a.S);
+  dim3 grid((a.S + qc - 1) / qc, n);
+  hipLaunchKernelGGL(attn_kernel<T>, grid, dim3(256), qc * a.S * sizeof(float), s, a);
+  return hipGetLastError();
+}
+template hipError_t launch_attn<float>(const AttnArgs&, int, hipStream_t);
+template hipError_t launch_attn<bf16_t>(const AttnArgs&, int, hipStream_t);
+
+// ============================================================================ head conv
+// head = Conv2d(3, ch, 3, padding=1) (Model.py:219) from the NCHW fp32 sampler state
+// to NHWC activations. One thread per (pixel, 4 output channels).
+template <typename T>
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  const int HW = a.H * a.W;
+  const int cq = a.Cout / 4;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)a.n * HW * cq;
+  if (idx >= total) return;
+  const int c4 = (int)(idx % cq);
+  const long long pix = idx / cq;
+  const int img = (int)(pix / HW);
+  const int rem = (int)(pix - (long long)img * HW);
+  const int y = rem / a.W, x = rem - y * a.W;
+  const float* xs = a.x + (size_t)(img % a.x_img_mod) * 3 * HW;
+  float in[27];
+#pragma unroll
+  for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = y + ky - 1, ix = x + kx - 1;
+        in[ci * 9 + ky * 3 + kx] = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? xs[ci * HW + iy * a.W + ix] : 0.0f;
+      }
+  float o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int co = c4 * 4 + e;
+    const float* w = a.w + co * 27;
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc = fmaf(w[k], in[k], acc);
+    o[e] = acc + a.b[co];
+  }
+  T* out = (T*)a.out + (size_t)pix * a.Cout + c4 * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[e] = Elem<T>::to(o[e]);
+}
+
+template <typename T>
+hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
+  const long long total = (long long)a.n * a.H * a.W * (a.Cout / 4);
+  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+template hipError_t launch_head<float>(const HeadArgs&, hipStream_t);
+template hipError_t launch_head<bf16_t>(const HeadArgs&, hipStream_t);
+
+// ============================================================================ Philox
+// Philox4x32-10 (Salmon et al., SC'11); normal via Box-Muller on the first two words.
+__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned step, unsigned long long idx) {
+  uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32), c2 = step, c3 = 0x1d5a1u;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  const float u1 = ((float)(c0 >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
+  const float u2 = (float)(c1 >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+
+// ============================================================================ tail conv + sampler step
+// tail = GN -> Swish -> Conv2d(C, 3, 3, padding=1) (Model.py:252-256, 282). The GN+Swish
+// output g is produced by groupnorm_kernel; this kernel does the 3-output conv per
+// pixel with the weights in LDS and then either writes eps (forward API) or applies
+// the ancestral update of Diffusion.py:67-71,96-100 in place on x:
+//   mean = coeff1[t]*x - coeff2[t]*eps ;  x = mean + sqrt(var[t]) * z  (z = 0 at t = 0)
+// CFG: eps = (1+w) eps_c - w eps_u (DiffusionCondition.py:85) with the unconditional
+// branch at image index img + n of g.
+template <typename T>
+__global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [9][C][3]
+  const int C = a.C;
+  for (int i = threadIdx.x; i < 27 * C; i += 256) {
+    // reference layout w[co][ci][ky][kx] -> wl[(tap*C + ci)*3 + co]
+    const int co = i / (C * 9);
+    const int r = i - co * C * 9;
+    const int ci = r / 9, tap = r - ci * 9;
+    wl[(tap * C + ci) * 3 + co] = a.w[i];
+  }
+  __syncthreads();
+  const int HW = a.H * a.W;
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (long long)a.n * HW) return;
+  const int img = (int)(pix / HW);
+  const int rem = (int)(pix - (long long)img * HW);
+  const int y = rem / a.W, x = rem - y * a.W;
+  auto conv3 = [&](int im, float& e0, float& e1, float& e2) {
+    const T* gb = (const T*)a.g + (size_t)im * HW * C;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = y + ky - 1;
+      if (iy < 0 || iy >= a.H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = x + kx - 1;
+        if (ix < 0 || ix >= a.W) continue;
+        const T* gp = gb + (size_t)(iy * a.W + ix) * C;
+        const float* wp = wl + (ky * 3 + kx) * C * 3;
+        for (int c = 0; c < C; c += EPC) {
+          const u32x4 v = *(const u32x4*)(gp + c);
+          const T* ve = (const T*)&v;
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            const float gv = Elem<T>::tof(ve[e]);
+            s0 = fmaf(gv, wp[(c + e) * 3 + 0], s0);
+            s1 = fmaf(gv, wp[(c + e) * 3 + 1], s1);
+            s2 = fmaf(gv, wp[(c + e) * 3 + 2], s2);
+          }
+        }
+      }
+    }
+    e0 = s0 + a.b[0]; e1 = s1 + a.b[1]; e2 = s2 + a.b[2];
+  };
+  float eps[3];
+  conv3(img, eps[0], eps[1], eps[2]);
+  if (a.cfg) {
+#pragma clang fp contract(off)
+    float u[3];
+    conv3(img + a.n, u[0], u[1], u[2]);
+    const float w1 = a.guide_w1;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) eps[c] = w1 * eps[c] - a.guide_w * u[c];
+  }
+  if (!a.step_mode) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.eps_out[((size_t)img * 3 + c) * HW + rem] = eps[c];
+    return;
+  }
+  {
+#pragma clang fp contract(off)
+    const int t = *a.tsel;
+    const float c1 = a.coeff1[t], c2 = a.coeff2[t], sv = a.sqrt_var[t];
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t o = ((size_t)img * 3 + c) * HW + rem;
+      const float xv = a.x[o];
+      const float mean = c1 * xv - c2 * eps[c];
+      float xn = mean;
+      if (t > 0) {
+        const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o] : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+        xn = mean + sv * z;
+      }
+      bad |= (xn != xn);
+      if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+      a.x[o] = xn;
+    }
+    if (bad) atomicOr(a.nan_flag, 1);
+  }
+}
+
+template <typename T>
+hipError_t launch_tail(const TailArgs& a, hipStream_t s) {
+  const long long total = (long long)a.n * a.H * a.W;
+  hipLaunchKernelGGL(tail_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 27 * a.C * sizeof(float), s, a);
+  return hipGetLastError();
+}
+template hipError_t launch_tail<float>(const TailArgs&, hipStream_t);
+template hipError_t launch_tail<bf16_t>(const TailArgs&, hipStream_t);
+
+// ============================================================================ embeddings
+// DDPM functional sinusoid (Model.py:74-88): e = interleave(sin(t f), cos(t f)).
+// CFG: row of a table (nn.Embedding, ModelCondition.py:38,54) selected by idx.
+__global__ void emb_input_kernel(const int* idx, int M, const float* freq, const float* table, int d, float* out,
+                                 int idx_offset) {
+  const int m = blockIdx.x;
+  if (m >= M) return;
+  const int t = idx ? idx[m] : (m + idx_offset);
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    float v;
+    if (table) v = table[(size_t)t * d + i];
+    else {
+      const float e = (float)t * freq[i >> 1];
+      v = (i & 1) ? cosf(e) : sinf(e);
+    }
+    out[(size_t)m * d + i] = v;
+  }
+}
+
+// out[m][j] = act_out( sum_i act_in(in[m][i]) * Wt[i][j] + b[j] ), Wt = W^T [Nin][Nout] fp32.
+__global__ __launch_bounds__(256) void linear_kernel(const float* in, int M, int Nin, const float* Wt, const float* b,
+                                                     int Nout, int silu_in, float* out) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int m = blockIdx.y;
+  extern __shared__ float xin[];
+  for (int i = threadIdx.x; i < Nin; i += 256) {
+    float v = in[(size_t)m * Nin + i];
+    xin[i] = silu_in ? silu(v) : v;
+  }
+  __syncthreads();
+  if (j >= Nout) return;
+  float acc = 0.0f;
+  for (int i = 0; i < Nin; ++i) acc = fmaf(xin[i], Wt[(size_t)i * Nout + j], acc);
+  out[(size_t)m * Nout + j] = acc + b[j];
+}
+
+hipError_t launch_emb_input(const int* idx, int M, const float* freq, const float* table, int d, float* out,
+                            int idx_offset, hipStream_t s) {
+  hipLaunchKernelGGL(emb_input_kernel, dim3(M), dim3(128), 0, s, idx, M, freq, table, d, out, idx_offset);
+  return hipGetLastError();
+}
+hipError_t launch_linear(const float* in, int M, int Nin, const float* Wt, const float* b, int Nout, int silu_in,
+                         float* out, hipStream_t s) {
+  hipLaunchKernelGGL(linear_kernel, dim3((Nout + 255) / 256, M), dim3(256), Nin * sizeof(float), s, in, M, Nin, Wt,
+                     b, Nout, silu_in, out);
+  return hipGetLastError();
+}
+
+// ============================================================================ verifiers
+// One block per candidate (b images of c*h*w). Reductions in fp64, then the fp32
+// roundings the reference performs (torch fp32 tensors, .item() to Python float).
+//  ORACLE    verifier.py:62-63   1/(1 + mean_b var_unbiased(x_b))
+//  AESTHETIC verifier.py:277-286 if min<0: x=(x+1)/2 ; 2 * mean_b std_unbiased(x_b)
+//  SELFSUP   verifier.py:219-246 avgpool 8x8 -> L2 normalise -> mean off-diagonal cosine
+__global__ __launch_bounds__(256) void verify_kernel(int kind, const float* images, int b, int c, int h, int w,
+                                                     double* scores) {
+  const int cand = blockIdx.x;
+  const int D = c * h * w;
+  const float* base = images + (size_t)cand * b * D;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ double red[4];
+  __shared__ double bc;
+  __shared__ float feat[64][192];  // selfsup: up to 64 images x (c*8*8 <= 192)
+  auto block_sum = [&](double v) -> double {
+    v = wave_sum_d(v);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  if (kind == 0 || kind == 2) {
+    bool shift = false;
+    if (kind == 2) {
+      float mn = INFINITY;
+      for (int i = tid; i < b * D; i += 256) mn = fminf(mn, base[i]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o, 64));
+      __syncthreads();
+      if (lane == 0) red[wid] = mn;
+      __syncthreads();
+      shift = fminf(fminf((float)red[0], (float)red[1]), fminf((float)red[2], (float)red[3])) < 0.0f;
+    }
+    float accum = 0.0f;  // fp32 mean over images, like a torch fp32 .mean()
+    for (int im = 0; im < b; ++im) {
+      const float* xb = base + (size_t)im * D;
+      double s = 0.0;
+      for (int i = tid; i < D; i += 256) {
+        float v = xb[i];
+        if (shift) v = (v + 1.0f) / 2.0f;
+        s += v;
+      }
+      const double mean = block_sum(s) / D;
+      double q = 0.0;
+      for (int i = tid; i < D; i += 256) {
+        float v = xb[i];
+        if (shift) v = (v + 1.0f) / 2.0f;
+        const double d = (double)v - mean;
+        q += d * d;
+      }
+      const double var = block_sum(q) / (D - 1);
+      accum += (kind == 0) ? (float)var : (float)sqrt(var);
+    }
+    if (tid == 0) {
+      const float m = accum / (float)b;
+      scores[cand] = (kind == 0) ? 1.0 / (1.0 + (double)m) : (double)(m + m);
+    }
+    return;
+  }
+  // SELFSUP: adaptive_avg_pool2d to 8x8 (h, w divisible by 8 here)
+  const int F = c * 64;
+  const int ph = h / 8, pw = w / 8;
+  for (int im = 0; im < b && im < 64; ++im) {
+    const float* xb = base + (size_t)im * D;
+    for (int f = tid; f < F; f += 256) {
+      const int ch = f / 64, cell = f % 64, cy = cell / 8, cx = cell % 8;
+      float s = 0.0f;
+      for (int yy = 0; yy < ph; ++yy)
+        for (int xx = 0; xx < pw; ++xx) s += xb[(size_t)ch * h * w + (cy * ph + yy) * w + cx * pw + xx];
+      feat[im][f] = s / (float)(ph * pw);
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && tid < b) {
+    double nn = 0.0;
+    for (int f = 0; f < F; ++f) nn += (double)feat[tid][f] * feat[tid][f];
+    const float nrm = fmaxf((float)sqrt(nn), 1e-12f);
+    for (int f = 0; f < F; ++f) feat[tid][f] = feat[tid][f] / nrm;
+  }
+  __syncthreads();
+  double s = 0.0;
+  for (int pr = tid; pr < b * b; pr += 256) {
+    const int i = pr / b, j = pr % b;
+    if (i == j) continue;
+    double d = 0.0;
+    for (int f = 0; f < F; ++f) d += (double)feat[i][f] * feat[j][f];
+    s += (double)(float)d;
+  }
+  s = block_sum(s);
+  if (tid == 0) {
+    const long long cnt = (long long)b * b - b;
+    bc = cnt > 0 ? s / (double)cnt : NAN;
+    scores[cand] = (double)(float)bc;
+  }
+}
+
+hipError_t launch_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w, double* scores,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(verify_kernel, dim3(n_cand), dim3(256), 0, s, kind, images, b, c, h, w, scores);
+  return hipGetLastError();
+}
+
+// out[c][e] = pivot[e] + scale * z(seed, stream_id, (cand_offset + c) * per_cand + e)
+__global__ __launch_bounds__(256) void noise_kernel(float* out, const float* pivot, long long total, long long per_cand,
+                                                    float scale, unsigned long long seed, unsigned stream_id,
+                                                    long long base) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const float z = philox_normal(seed, stream_id, (unsigned long long)(base + i));
+  out[i] = (pivot ? pivot[i % per_cand] : 0.0f) + scale * z;
+}
+hipError_t launch_noise(float* out, const float* pivot, int n_cand, long long per_cand, float scale,
+                        unsigned long long seed, unsigned stream_id, long long cand_offset, hipStream_t s) {
+  const long long total = (long long)n_cand * per_cand;
+  hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, pivot, total, per_cand,
+                     scale, seed, stream_id, cand_offset * per_cand);
+  return hipGetLastError();
+}
+
+// ============================================================================ small utilities
+__global__ void set_int_kernel(int* p, int v) { *p = v; }
+__global__ void add_int_kernel(int* p, int v) { *p += v; }
+hipError_t launch_set_int(int* p, int v, hipStream_t s) {
+  hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
+  return hipGetLastError();
+}
+hipError_t launch_add_int(int* p, int v, hipStream_t s) {
+  hipLaunchKernelGGL(add_int_kernel, dim3(1), dim3(1), 0, s, p, v);
+  return hipGetLastError();
+}
+
+}  // namespace itsd

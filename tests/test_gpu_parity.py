@@ -1,0 +1,218 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference-pinned fixtures and
+the CPU oracle on the same seeded inputs.
+
+Tolerances ("Parity"):
+  fp32 mode  per-forward eps   max|d| <= 2e-4          (f32 MFMA, different summation order)
+             trajectories x0   max|d| <= 2e-3          (T <= 20, injected reference noise)
+  bf16 mode  per-forward eps   rel-L2  <= 2e-2
+  verifiers                    |d| <= 1e-5 (NaN where the reference gives NaN)
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ref_cpu as R
+from itsd.arch import ARCH_A, ARCH_TINY, ARCH_TINY_CFG
+from itsd.diffusion import CondGaussianDiffusionSampler, GaussianDiffusionSampler, reference_noise_plan
+from itsd.model import CondUNet, UNet
+from itsd.search import SearchEngine
+from itsd.verifier import AestheticPredictor, OracleVerifier, SelfSupervisedVerifier
+from itsd.weights import synthetic_state_dict
+from itsd import runtime as rt
+
+pytestmark = pytest.mark.gpu
+
+EPS_TOL_FP32 = 2e-4
+TRAJ_TOL_FP32 = 2e-3
+REL_L2_BF16 = 2e-2
+
+
+def _net(a, precision="fp32", seed=0):
+    if a.cfg:
+        net = CondUNet(a.T, a.num_labels, a.ch, a.ch_mult, a.num_res_blocks, 0.0, precision=precision)
+    else:
+        net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=precision)
+    net.load_state_dict(synthetic_state_dict(a, seed))
+    return net.to("cuda:0")
+
+
+def _oracle(a, sd):
+    return lambda x, t, labels=None: R.unet_forward(sd, x, t, a.ch, a.ch_mult, a.attn, a.num_res_blocks,
+                                                    labels=labels, cfg=a.cfg)
+
+
+def _rel_l2(a, b):
+    return (torch.linalg.norm((a - b).flatten()) / torch.linalg.norm(b.flatten())).item()
+
+
+def test_native_lib_is_loaded(gpu_lib):
+    assert gpu_lib.itsd_version() == 1
+
+
+@pytest.mark.parametrize("arch,fix", [(ARCH_TINY, "tiny_ddpm_eps"), (ARCH_A, "archA_eps")])
+def test_forward_fp32_vs_reference(arch, fix):
+    g = golden(fix)
+    net = _net(arch)
+    eps = net(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["t"]).cuda()).cpu().numpy()
+    np.testing.assert_allclose(eps, g["eps"], atol=EPS_TOL_FP32, rtol=0)
+
+
+def test_forward_cfg_fp32_vs_reference():
+    g = golden("tiny_cfg_eps")
+    net = _net(ARCH_TINY_CFG)
+    eps = net(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["t"]).cuda(),
+              torch.from_numpy(g["labels"]).cuda()).cpu().numpy()
+    np.testing.assert_allclose(eps, g["eps"], atol=EPS_TOL_FP32, rtol=0)
+
+
+@pytest.mark.parametrize("n", [1, 3, 8])
+def test_forward_bf16_archA_vs_oracle(n):
+    a = ARCH_A
+    sd = synthetic_state_dict(a, 0)
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    eps = net(x.cuda(), t.cuda()).cpu()
+    with torch.no_grad():
+        ref = _oracle(a, sd)(x, t)
+    assert _rel_l2(eps, ref) < REL_L2_BF16
+
+
+def test_trajectory_tiny_fp32_vs_reference():
+    g = golden("tiny_ddpm_traj")
+    T = int(g["T"])
+    net = _net(ARCH_TINY)
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
+    noise = torch.cat([torch.zeros(1, 2, 3, 32, 32), torch.from_numpy(g["noise"]).flip(0)])  # [T] by step t
+    for graph in (True, False):
+        x0 = smp(torch.from_numpy(g["x_T"]).cuda(), noise=noise, graph=graph).cpu().numpy()
+        np.testing.assert_allclose(x0, g["x0"], atol=TRAJ_TOL_FP32, rtol=0)
+
+
+def test_trajectory_cfg_fp32_vs_reference():
+    g = golden("tiny_cfg_traj")
+    T = int(g["T"])
+    net = _net(ARCH_TINY_CFG)
+    smp = CondGaussianDiffusionSampler(net, 1e-4, 0.028, T, w=float(g["w"]))
+    noise = torch.cat([torch.zeros(1, 2, 3, 32, 32), torch.from_numpy(g["noise"]).flip(0)])
+    x0 = smp(torch.from_numpy(g["x_T"]).cuda(), torch.from_numpy(g["labels"]).cuda(), noise=noise).cpu().numpy()
+    np.testing.assert_allclose(x0, g["x0"], atol=TRAJ_TOL_FP32, rtol=0)
+
+
+def test_trajectory_archA_fp32_vs_reference():
+    g = golden("archA_traj")
+    T = int(g["T"])
+    torch.manual_seed(int(g["seed"]))
+    x_T, noise = reference_noise_plan((2, 3, 32, 32), T, n_runs=1)
+    net = _net(ARCH_A)
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
+    x0 = smp(x_T[0].cuda(), noise=noise).cpu().numpy()
+    np.testing.assert_allclose(x0, g["x0"], atol=TRAJ_TOL_FP32, rtol=0)
+
+
+def test_verifiers_vs_reference():
+    g = golden("verifiers")
+    for case in ("b1_neg", "b4_neg", "b4_pos", "b2_neg"):
+        im = torch.from_numpy(g[case + "_images"]).cuda()
+        for name, V in (("oracle", OracleVerifier()), ("selfsup", SelfSupervisedVerifier()),
+                        ("aesthetic", AestheticPredictor())):
+            want = float(g[f"{case}_{name}"])
+            got = V.score(im)
+            if math.isnan(want):
+                assert math.isnan(got), (case, name)
+            else:
+                assert abs(got - want) <= 1e-5, (case, name, got, want)
+
+
+def test_verifier_batched_equals_per_candidate():
+    gen = torch.Generator().manual_seed(9)
+    im = (torch.randn(12, 3, 32, 32, generator=gen) * 0.5).clamp(-1, 1)
+    im[8:] = im[8:].abs()  # candidates without negatives take the other aesthetic branch
+    for V in (OracleVerifier(), SelfSupervisedVerifier(), AestheticPredictor()):
+        batch = V.score_batch(im.cuda(), 4).cpu()
+        for c in range(4):
+            ref = R.VERIFIERS[{0: "oracle", 1: "selfsup", 2: "aesthetic"}[V.kind]](im[3 * c:3 * c + 3])
+            assert abs(batch[c].item() - ref) <= 1e-5
+
+
+def test_search_outcomes_match_reference_T5():
+    """RandomSearch / ZeroOrder / PathSearch on the tiny UNet, T=5, seeds of the golden
+    run: candidates batched into one native sampler run with the reference's noise."""
+    g = golden("search_T5")
+    T = 5
+    net = _net(ARCH_TINY)
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
+    ver = OracleVerifier()
+    shape = (1, 3, 32, 32)
+
+    # RandomSearch(4): per candidate randn(noise) then T-1 step draws (search_algorithm.py:65-75)
+    torch.manual_seed(0)
+    x_T, noise = reference_noise_plan(shape, T, n_runs=4)
+    x = smp(x_T.reshape(4, 3, 32, 32).cuda(), noise=noise)
+    scores = ver.score_batch(x, 4).cpu().numpy()
+    np.testing.assert_allclose(scores, g["random_scores"], atol=1e-5)
+    assert int(np.argmax(scores)) == int(np.argmax(g["random_scores"]))
+    np.testing.assert_array_equal(x_T[int(np.argmax(scores))].numpy(), g["random_best_noise"])
+
+    # ZeroOrder(3 neighbours, 2 iterations): neighbours drawn first, then each one's T-1 draws
+    torch.manual_seed(1)
+    pivot = torch.randn(shape)
+    best_score, best_noise = float("-inf"), pivot
+    for it in range(2):
+        neigh = torch.stack([pivot + torch.randn_like(pivot) * (1 - 0.95) for _ in range(3)])
+        zs = []
+        for _ in range(3):
+            zs.append(torch.stack([torch.randn(shape) for _ in range(T - 1)] + [torch.zeros(shape)]).flip(0))
+        noise = torch.stack(zs, dim=1).reshape(T, 3, 3, 32, 32)
+        x = smp(neigh.reshape(3, 3, 32, 32).cuda(), noise=noise)
+        sc = ver.score_batch(x, 3).cpu().numpy()
+        np.testing.assert_allclose(sc, g["zo_scores"][it], atol=1e-5)
+        if sc.max() > best_score:  # search_algorithm.py:193-196
+            best_score, best_noise = float(sc.max()), neigh[int(np.argmax(sc))]
+            pivot = best_noise
+    np.testing.assert_allclose(best_noise.numpy(), g["zo_best_noise"], atol=1e-6)
+    assert abs(best_score - float(g["zo_best_score"])) < 1e-5
+
+
+def test_noise_generator_statistics_and_sharding():
+    out = torch.empty(64, 3, 32, 32, device="cuda")
+    rt.noise(out, 64, seed=123, stream_id=7)
+    z = out.cpu()
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1) < 0.01
+    # candidate noise depends only on its global index: a shard regenerates the same values
+    part = torch.empty(16, 3, 32, 32, device="cuda")
+    rt.noise(part, 16, seed=123, stream_id=7, cand_offset=32)
+    assert torch.equal(part.cpu(), z[32:48])
+
+
+def test_batch_invariance_and_sampler_determinism_bf16():
+    """A candidate's trajectory is a function of (seed, global index) only: running it
+    in a batch of 8 or as the second shard of 4 gives bit-identical results."""
+    a = ARCH_TINY
+    net = _net(a, "bf16")
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, 1000)
+    x = torch.empty(8, 3, 32, 32, device="cuda")
+    rt.noise(x, 8, seed=5, stream_id=0xF0000000)
+    full = smp.run(x.clone(), t_begin=999, t_end=990, seed=77)
+    per = x[0].numel()
+    half = smp.run(x[4:].clone(), t_begin=999, t_end=990, seed=77, noise_offset=4 * per)
+    assert torch.equal(full[4:], half)
+    again = smp.run(x.clone(), t_begin=999, t_end=990, seed=77, graph=False)
+    assert torch.equal(full, again)
+
+
+def test_engine_random_search_full_T_archA_bf16():
+    """The benchmark path at small N: 8 candidates x T=1000 on Arch A in bf16; finite,
+    clipped, and the reported best is the argmax of the scores."""
+    net = _net(ARCH_A, "bf16")
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, 1000)
+    eng = SearchEngine(smp, OracleVerifier(), seed=1)
+    best_noise, best_score, info = eng.random_search(8, (1, 3, 32, 32))
+    sc = torch.tensor(info["scores"])
+    assert torch.isfinite(sc).all()
+    assert best_score == sc.max().item() and info["best_index"] == int(torch.argmax(sc))
+    assert best_noise.shape == (1, 3, 32, 32)

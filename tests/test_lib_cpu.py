@@ -1,0 +1,71 @@
+"""CPU-side checks of the boundary: the C-ABI library loads and exports every
+symbol include/itsd.h declares; host-side helpers behave (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+import itsd
+from itsd import runtime as rt
+from itsd.arch import ARCH_A, ARCH_C, ARCH_TINY, flops_per_image, param_specs
+from itsd.diffusion import reference_noise_plan
+from itsd.weights import check_state_dict, synthetic_state_dict
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "itsd.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(itsd_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    if not os.path.exists(rt.LIB_PATH):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    L = ctypes.CDLL(rt.LIB_PATH)
+    syms = _header_symbols()
+    assert len(syms) >= 9
+    for s in syms:
+        assert hasattr(L, s), f"missing export {s}"
+    assert set(syms) == set(rt.EXPORTS), "runtime.py bindings out of sync with include/itsd.h"
+    assert L.itsd_version() == 1
+
+
+def test_param_specs_match_reference_key_counts():
+    # Arch A has 333 keys, Arch C 614
+    assert len(param_specs(ARCH_A)) == 333
+    assert len(param_specs(ARCH_C)) == 614
+
+
+def test_flops_archA():
+    # 14.882 GFLOP per 32px image forward (FlopCounterMode)
+    assert abs(flops_per_image(ARCH_A) / 1e9 - 14.882) < 0.01
+
+
+def test_state_dict_checks():
+    sd = synthetic_state_dict(ARCH_TINY, 0)
+    check_state_dict(ARCH_TINY, sd)
+    bad = dict(sd)
+    bad.pop("head.weight")
+    with pytest.raises(KeyError):
+        check_state_dict(ARCH_TINY, bad)
+    bad = dict(sd)
+    bad["head.bias"] = torch.zeros(3)
+    with pytest.raises(ValueError):
+        check_state_dict(ARCH_TINY, bad)
+
+
+def test_reference_noise_plan_order():
+    torch.manual_seed(3)
+    x_T, noise = reference_noise_plan((1, 3, 4, 4), T=4, n_runs=2)
+    torch.manual_seed(3)
+    seq = [torch.randn(1, 3, 4, 4) for _ in range(2 * 4)]
+    # run 0: x_T, z(t=3), z(2), z(1); run 1: x_T, z(3), z(2), z(1)
+    assert torch.equal(x_T[0], seq[0]) and torch.equal(x_T[1], seq[4])
+    for run in range(2):
+        for k, t in enumerate([3, 2, 1]):
+            assert torch.equal(noise[t, run], seq[4 * run + 1 + k][0])
+    assert torch.count_nonzero(noise[0]) == 0
