@@ -25,6 +25,7 @@
 namespace itsd {
 template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
 template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
+template <typename T> hipError_t launch_stats(const void*, int, int, int, float*, hipStream_t);
 template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
@@ -72,6 +73,7 @@ uint16_t host_f2bf(float f) {
 struct Act {
   size_t off;
   int H, W, C;
+  size_t stats = SIZE_MAX;  // ws offset of the channel-statistics slab (consumed by a GroupNorm), or none
 };
 
 enum OpKind { OP_GN, OP_CONV, OP_ATTN };
@@ -431,6 +433,29 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
     return fail(ITSD_ERR_WEIGHTS, "state_dict has " + std::to_string(nviews) + " entries, model uses " +
                                       std::to_string(b.used) + " (unexpected keys present)");
   }
+  // channel-statistics slabs for every tensor a GroupNorm reads (written by its producer)
+  {
+    std::vector<int> need;
+    for (const Op& o : u->ops)
+      if (o.kind == OP_GN) {
+        need.push_back(o.src1);
+        if (o.src2 >= 0) need.push_back(o.src2);
+      }
+    need.push_back(u->tail_in);
+    for (int id : need) {
+      Act& A = u->acts[id];
+      if (A.stats != SIZE_MAX) continue;
+      const int HW = A.H * A.W;
+      if (!(128 % HW == 0 || HW % 128 == 0))
+        return fail(ITSD_ERR_INVALID, "spatial size " + std::to_string(HW) + " not supported by the GN statistics slots");
+      const size_t slots = (size_t)u->nb_max * HW / stat_slot_px(HW);
+      A.stats = b.ws_off;
+      b.ws_off = (b.ws_off + slots * 2 * A.C * 4 + 255) & ~(size_t)255;
+      bool produced = (id == u->head_out);
+      for (const Op& o : u->ops) produced |= (o.kind == OP_CONV && o.dst == id);
+      if (!produced) return fail(ITSD_ERR_INVALID, "internal: GroupNorm input without a statistics producer");
+    }
+  }
   // device arenas
   HIPCHK(hipMalloc(&u->wdev, b.ar.host.size()));
   HIPCHK(hipMemcpy(u->wdev, b.ar.host.data(), b.ar.host.size(), hipMemcpyHostToDevice));
@@ -472,6 +497,8 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.eps = 1e-5f;
     a.silu = o.silu;
     a.dst = u->ap(o.dst);
+    a.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
+    a.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
     e = u->bf16 ? launch_groupnorm<bf16_t>(a, c.nb, s) : launch_groupnorm<float>(a, c.nb, s);
   } else if (o.kind == OP_CONV) {
     ConvArgs a{};
@@ -502,6 +529,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.resid = o.resid >= 0 ? u->ap(o.resid) : nullptr;
     a.out = u->ap(o.dst);
     a.M = c.nb * out.H * out.W;
+    a.stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.zins = o.zins;
     {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
       const int epc = u->bf16 ? 8 : 4;
@@ -553,6 +581,12 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     h.out = u->ap(u->head_out);
     h.H = u->H; h.W = u->H; h.Cout = u->ch; h.n = c.nb; h.x_img_mod = c.x_mod;
     hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
+    const Act& ho = u->acts[u->head_out];
+    if (e == hipSuccess && ho.stats != SIZE_MAX) {
+      float* st = (float*)(u->ws + ho.stats);
+      e = u->bf16 ? launch_stats<bf16_t>(h.out, c.nb * u->H * u->H, u->ch, u->H * u->H, st, s)
+                  : launch_stats<float>(h.out, c.nb * u->H * u->H, u->ch, u->H * u->H, st, s);
+    }
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   for (const Op& o : u->ops) CHK(mark((int)o.kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));

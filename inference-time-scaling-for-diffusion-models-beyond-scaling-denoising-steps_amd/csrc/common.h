@@ -74,15 +74,22 @@ struct ConvArgs {
   const void* resid;                 // [M][Cout] same layout as out, or null
   void* out;                         // [M][Cout]
   int M;                             // n * Hout * Wout
+  float* stats;                      // channel-statistics slab [slot][2][Cout] for the consumer GN, or null
 };
+
+// Channel-statistics slab of an NHWC tensor (written by its producer): slots of
+// Gt = min(HW, 128) consecutive pixels; stats[slot][0][c] = sum, [slot][1][c] = sum of squares.
+__host__ __device__ inline int stat_slot_px(int HW) { return HW < 128 ? HW : 128; }
 
 struct GNArgs {
   const void* src1; const void* src2;  // NHWC, C1 (+ C2) channels
+  const float* st1; const float* st2;  // their statistics slabs
   int C1, C2, HW;
   const float* gamma; const float* beta;
   float eps;
   int silu;
   void* dst;                           // NHWC, C1+C2 channels
+  int chunks_per_block;                // 16-B chunks of one image handled per block
 };
 
 struct AttnArgs {

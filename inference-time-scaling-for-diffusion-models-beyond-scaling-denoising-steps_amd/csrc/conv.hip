@@ -13,7 +13,8 @@
 // (row>>1)&7, which makes the per-lane ds_read_b128 fragment reads conflict-free.
 // K loop: register-staged double buffer (global loads of stage k+1 are in flight
 // while stage k's MFMAs run), one barrier per stage.
-// Epilogue fuses + bias + temb_proj row (+ CFG cond_proj row) + residual.
+// Epilogue (LDS-staged) fuses + bias + temb_proj row (+ CFG cond_proj row) + residual,
+// stores coalesced 16-B chunks and emits the consumer GroupNorm's channel statistics.
 #include "common.h"
 
 namespace itsd {
@@ -22,6 +23,8 @@ constexpr int CONV_BM = 128;  // couts per block
 constexpr int CONV_BN = 128;  // pixels per block
 constexpr int ROWB = 128;     // bytes per LDS row
 constexpr int TILEB = 128 * ROWB;
+constexpr int EROW = 132;  // epilogue LDS row (floats)
+constexpr int SMEM_BYTES = (2 * 2 * TILEB > 128 * EROW * 4) ? 2 * 2 * TILEB : 128 * EROW * 4;
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -29,7 +32,7 @@ template <typename T>
 __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B chunk
   constexpr int BK = 8 * EPC;               // k per stage
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILEB];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -160,62 +163,97 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs a) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+  // 1. accumulators -> fp32 tile in LDS [pixel][cout] (row pad 4 floats: conflict-free)
+  // 2. fused bias + temb/cemb rows + residual, rounded and stored as full 16-B chunks
+  //    (coalesced rows of the NHWC output), rounded values written back to LDS
+  // 3. per-channel (sum, sum of squares) over each pixel slot of the tile: the
+  //    GroupNorm statistics of the consumer (Model.py:171,180), written as a
+  //    deterministic partial slab stats[slot][2][Cout] (no atomics).
+  float* E = (float*)smem;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int p = tileP + wn * 64 + j * 32 + rl;
-    if (p >= a.M) continue;
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
+      }
+  __syncthreads();
+  const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+  constexpr int CPR = 128 / EPC;  // 16-B output chunks per tile row
+  for (int it = tid; it < 128 * CPR; it += 256) {
+    const int pl = it / CPR, cl = (it - pl * CPR) * EPC;
+    const int p = tileP + pl, co = tileC + cl;
+    if (p >= a.M || co >= a.Cout) continue;
     const int img = p / HWo;
-    const float* tb = a.temb ? a.temb + trow + (long long)img * a.temb_img_stride : nullptr;
-    const float* cb = nullptr;
+    float v[EPC];
+#pragma unroll
+    for (int q = 0; q < EPC / 4; ++q) {
+      const f32x4 e4 = *(const f32x4*)(E + pl * EROW + cl + 4 * q);
+      const f32x4 b4 = *(const f32x4*)(a.bias + co + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
+    }
+    if (a.temb) {
+      const float* tb = a.temb + trow + (long long)img * a.temb_img_stride + co;
+#pragma unroll
+      for (int q = 0; q < EPC / 4; ++q) {
+        const f32x4 t4 = *(const f32x4*)(tb + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] += t4[e];
+      }
+    }
     if (a.cemb) {
       int lab = 0;
       if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-      cb = a.cemb + (long long)lab * a.cemb_row_stride;
-    }
+      const float* cb = a.cemb + (long long)lab * a.cemb_row_stride + co;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+      for (int q = 0; q < EPC / 4; ++q) {
+        const f32x4 c4 = *(const f32x4*)(cb + 4 * q);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co = tileC + wm * 64 + i * 32 + 8 * g + 4 * hh;
-        if (co >= a.Cout) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * g + e];
-        const f32x4 bb = *(const f32x4*)(a.bias + co);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bb[e];
-        if (tb) {
-          const f32x4 t4 = *(const f32x4*)(tb + co);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += t4[e];
-        }
-        if (cb) {
-          const f32x4 c4 = *(const f32x4*)(cb + co);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += c4[e];
-        }
-        const size_t o = (size_t)p * a.Cout + co;
-        if constexpr (sizeof(T) == 2) {
-          if (a.resid) {
-            const uint2 r2 = *(const uint2*)((const bf16_t*)a.resid + o);
-            v[0] += bf2f((bf16_t)(r2.x & 0xffff)); v[1] += bf2f((bf16_t)(r2.x >> 16));
-            v[2] += bf2f((bf16_t)(r2.y & 0xffff)); v[3] += bf2f((bf16_t)(r2.y >> 16));
-          }
-          uint2 w2;
-          w2.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          w2.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *(uint2*)((bf16_t*)a.out + o) = w2;
-        } else {
-          if (a.resid) {
-            const f32x4 r4 = *(const f32x4*)((const float*)a.resid + o);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += r4[e];
-          }
-          f32x4 w4 = {v[0], v[1], v[2], v[3]};
-          *(f32x4*)((float*)a.out + o) = w4;
-        }
+        for (int e = 0; e < 4; ++e) v[4 * q + e] += c4[e];
       }
+    }
+    const size_t o = (size_t)p * a.Cout + co;
+    if (a.resid) {
+      const u32x4 r = *(const u32x4*)((const T*)a.resid + o);
+      const T* re = (const T*)&r;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) v[e] += Elem<T>::tof(re[e]);
+    }
+    u32x4 w;
+    T* we = (T*)&w;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(v[e]);
+    *(u32x4*)((T*)a.out + o) = w;
+    if (a.stats) {
+#pragma unroll
+      for (int q = 0; q < EPC / 4; ++q) {
+        f32x4 s4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s4[e] = Elem<T>::tof(we[4 * q + e]);
+        *(f32x4*)(E + pl * EROW + cl + 4 * q) = s4;
+      }
+    }
+  }
+  if (a.stats) {
+    __syncthreads();
+    const int Gt = HWo < 128 ? HWo : 128;  // pixels per slot (host guarantees 128 % HWo == 0 or HWo % 128 == 0)
+    const int S = 128 / Gt;
+    for (int item = tid; item < S * 128; item += 256) {
+      const int s = item >> 7, cl = item & 127;
+      const int co = tileC + cl, p0 = tileP + s * Gt;
+      if (co >= a.Cout || p0 >= a.M) continue;
+      float sum = 0.f, sq = 0.f;
+      for (int k = 0; k < Gt; ++k) {
+        const float v = E[(s * Gt + k) * EROW + cl];
+        sum += v;
+        sq = fmaf(v, v, sq);
+      }
+      const long long slot = p0 / Gt;
+      a.stats[(slot * 2) * a.Cout + co] = sum;
+      a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
     }
   }
 }

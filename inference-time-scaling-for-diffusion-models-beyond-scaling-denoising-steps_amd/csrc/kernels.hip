@@ -9,64 +9,117 @@
 namespace itsd {
 
 // ============================================================================ GroupNorm
-// nn.GroupNorm(32, C, eps=1e-5) (Model.py:132,171,180,253) with optional Swish, over
+// nn.GroupNorm(32, C, eps=1e-5) (Model.py:132,171,180,253) with optional Swish over
 // the channel concat of two NHWC sources (the up path's torch.cat, Model.py:280; a
-// group may straddle the two sources). One block per (group, image); two-pass
-// mean / biased variance in fp64, then y = x*a + b with a = rstd*gamma,
-// b = beta - mean*a written to a contiguous NHWC buffer of C1+C2 channels.
+// group may straddle the two sources). The statistics come from the producers'
+// channel slabs (conv epilogue / stats_kernel): per image, the group's sum and sum
+// of squares are reduced in fp64 (fixed order: deterministic), mean/biased var ->
+// a = rstd*gamma, b = beta - mean*a per channel in LDS; the block then streams its
+// pixel range with 16-B loads/stores: y = silu(x*a + b).
 template <typename T>
-__global__ __launch_bounds__(256) void groupnorm_kernel(GNArgs a) {
-  const int g = blockIdx.x, img = blockIdx.y;
-  const int C = a.C1 + a.C2;
-  const int gs = C / 32;
-  const int E = gs * a.HW;
+__global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  __shared__ float coef[2][2048];
+  __shared__ float gst[32][2];
+  const int img = blockIdx.y, tid = threadIdx.x;
+  const int C = a.C1 + a.C2, gs = C / 32;
+  const int Gt = stat_slot_px(a.HW), spi = a.HW / Gt;
+  {
+    const int g = tid >> 3, l8 = tid & 7;
+    double s = 0.0, q = 0.0;
+    for (int k = l8; k < gs * spi; k += 8) {
+      const int c = g * gs + k / spi;
+      const long long sl = (long long)img * spi + (k % spi);
+      const float* st;
+      int Cs, cc;
+      if (c < a.C1) { st = a.st1; Cs = a.C1; cc = c; } else { st = a.st2; Cs = a.C2; cc = c - a.C1; }
+      s += (double)st[(sl * 2) * Cs + cc];
+      q += (double)st[(sl * 2 + 1) * Cs + cc];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+    if (l8 == 0) {
+      const double E = (double)gs * a.HW;
+      const double mean = s / E;
+      double var = q / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      gst[g][0] = (float)mean;
+      gst[g][1] = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int g = c / gs;
+    const float sc = gst[g][1] * a.gamma[c];
+    coef[0][c] = sc;
+    coef[1][c] = a.beta[c] - gst[g][0] * sc;
+  }
+  __syncthreads();
+  const int cpp = C / EPC;  // chunks per pixel
+  const long long total = (long long)a.HW * cpp;
+  const long long c0 = (long long)blockIdx.x * a.chunks_per_block;
+  const long long c1 = min(total, c0 + a.chunks_per_block);
   const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
   const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
   T* dst = (T*)a.dst + (size_t)img * a.HW * C;
-  __shared__ double red[4];
-  __shared__ float stat[2];
-  auto ld = [&](int e, int& p, int& c) -> float {
-    p = e / gs;
-    c = g * gs + (e - p * gs);
-    return c < a.C1 ? Elem<T>::tof(s1[(size_t)p * a.C1 + c]) : Elem<T>::tof(s2[(size_t)p * a.C2 + (c - a.C1)]);
-  };
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  double s = 0.0;
-  for (int e = tid; e < E; e += 256) { int p, c; s += (double)ld(e, p, c); }
-  s = wave_sum_d(s);
-  if (lane == 0) red[wid] = s;
-  __syncthreads();
-  const double mean = (red[0] + red[1] + red[2] + red[3]) / (double)E;
-  __syncthreads();
-  double q = 0.0;
-  for (int e = tid; e < E; e += 256) { int p, c; const double d = (double)ld(e, p, c) - mean; q += d * d; }
-  q = wave_sum_d(q);
-  if (lane == 0) red[wid] = q;
-  __syncthreads();
-  if (tid == 0) {
-    const double var = (red[0] + red[1] + red[2] + red[3]) / (double)E;
-    stat[0] = (float)mean;
-    stat[1] = (float)(1.0 / sqrt(var + (double)a.eps));
-  }
-  __syncthreads();
-  const float mf = stat[0], rstd = stat[1];
-  for (int e = tid; e < E; e += 256) {
-    int p, c;
-    const float x = ld(e, p, c);
-    const float sc = rstd * a.gamma[c];
-    float y = x * sc + (a.beta[c] - mf * sc);
-    if (a.silu) y = silu(y);
-    dst[(size_t)p * C + c] = Elem<T>::to(y);
+  for (long long idx = c0 + tid; idx < c1; idx += 256) {
+    const int p = (int)(idx / cpp);
+    const int c = (int)(idx - (long long)p * cpp) * EPC;
+    const u32x4 x = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c)
+                             : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
+    const T* xe = (const T*)&x;
+    u32x4 y;
+    T* ye = (T*)&y;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      float v = Elem<T>::tof(xe[e]) * coef[0][c + e] + coef[1][c + e];
+      if (a.silu) v = silu(v);
+      ye[e] = Elem<T>::to(v);
+    }
+    *(u32x4*)(dst + (size_t)p * C + c) = y;
   }
 }
 
 template <typename T>
-hipError_t launch_groupnorm(const GNArgs& a, int n, hipStream_t s) {
-  hipLaunchKernelGGL(groupnorm_kernel<T>, dim3(32, n), dim3(256), 0, s, a);
+hipError_t launch_groupnorm(const GNArgs& a0, int n, hipStream_t s) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  GNArgs a = a0;
+  const long long total = (long long)a.HW * ((a.C1 + a.C2) / EPC);
+  a.chunks_per_block = 1024;
+  const int bpi = (int)((total + a.chunks_per_block - 1) / a.chunks_per_block);
+  hipLaunchKernelGGL(gn_apply_kernel<T>, dim3(bpi, n), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 template hipError_t launch_groupnorm<float>(const GNArgs&, int, hipStream_t);
 template hipError_t launch_groupnorm<bf16_t>(const GNArgs&, int, hipStream_t);
+
+// Channel-statistics slab of an NHWC tensor that no conv epilogue produced (the head
+// output): one block per slot of Gt pixels, one thread per channel.
+template <typename T>
+__global__ __launch_bounds__(256) void stats_kernel(const T* x, int M, int C, int HW, float* stats) {
+  const int Gt = stat_slot_px(HW);
+  const long long slot = blockIdx.x;
+  const long long p0 = slot * Gt;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f, q = 0.f;
+    for (int k = 0; k < Gt && p0 + k < M; ++k) {
+      const float v = Elem<T>::tof(x[(size_t)(p0 + k) * C + c]);
+      s += v;
+      q = fmaf(v, v, q);
+    }
+    stats[(slot * 2) * C + c] = s;
+    stats[(slot * 2 + 1) * C + c] = q;
+  }
+}
+
+template <typename T>
+hipError_t launch_stats(const void* x, int M, int C, int HW, float* stats, hipStream_t s) {
+  const int Gt = stat_slot_px(HW);
+  hipLaunchKernelGGL(stats_kernel<T>, dim3((M + Gt - 1) / Gt), dim3(256), 0, s, (const T*)x, M, C, HW, stats);
+  return hipGetLastError();
+}
+template hipError_t launch_stats<float>(const void*, int, int, int, float*, hipStream_t);
+template hipError_t launch_stats<bf16_t>(const void*, int, int, int, float*, hipStream_t);
 
 // ============================================================================ attention core
 // AttnBlock core (Model.py:152-161): w = softmax(q k^T * C^-0.5) ; h = w v, single head,

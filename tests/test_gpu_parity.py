@@ -212,7 +212,7 @@ def test_engine_random_search_full_T_archA_bf16():
     smp = GaussianDiffusionSampler(net, 1e-4, 0.02, 1000)
     eng = SearchEngine(smp, OracleVerifier(), seed=1)
     best_noise, best_score, info = eng.random_search(8, (1, 3, 32, 32))
-    sc = torch.tensor(info["scores"])
+    sc = torch.tensor(info["scores"], dtype=torch.float64)
     assert torch.isfinite(sc).all()
     assert best_score == sc.max().item() and info["best_index"] == int(torch.argmax(sc))
     assert best_noise.shape == (1, 3, 32, 32)
