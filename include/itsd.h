@@ -121,6 +121,13 @@ int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, 
 int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, double* conv_ms,
                          double* conv_flops, int* conv_launches, double* total_ms, void* stream);
 
+/* Per-launch census of one forward (synchronous, eager, HIP events): for launch i
+ * (head, program ops in order, tail GN, tail) kinds[i] (0 GN, 1 conv, 2 attention,
+ * -1 head, -2 tail), ms[i], flops[i] and shapes[6*i..] = {M, Cout, K or Cin, Hout,
+ * ksize, 10*stride+upsample}. At most max_ops entries; *n_ops = entries written. */
+int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
+                     double* ms, double* flops, int* shapes, int* n_ops, void* stream);
+
 const char* itsd_last_error(void);
 int itsd_version(void);
 

@@ -150,6 +150,7 @@ struct itsd_unet {
   float guide_w = 0.f, guide_w1 = 1.f;
   int* d_t = nullptr;
   int* d_nan = nullptr;
+  void* zero_page = nullptr;  // 1 KiB of zeros (conv DMA source for padding)
 
   hipStream_t stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -530,6 +531,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.out = u->ap(o.dst);
     a.M = c.nb * out.H * out.W;
     a.stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
+    a.zero = u->zero_page;
     a.zins = o.zins;
     {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
       const int epc = u->bf16 ? 8 : 4;
@@ -689,6 +691,8 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipEventCreateWithFlags(&u->ev_out, hipEventDisableTiming));
   HIPCHK(hipMalloc(&u->d_t, 64));
   HIPCHK(hipMalloc(&u->d_nan, 64));
+  HIPCHK(hipMalloc(&u->zero_page, 1024));
+  HIPCHK(hipMemset(u->zero_page, 0, 1024));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -706,7 +710,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   clear_graphs(u);
   hipFree(u->wdev); hipFree(u->ws); hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
   hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
-  hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan);
+  hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->zero_page);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
   if (u->ev_out) hipEventDestroy(u->ev_out);
@@ -880,6 +884,63 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
   if (conv_flops) *conv_flops = cf;
   if (conv_launches) *conv_launches = cl;
   if (total_ms) *total_ms = tm;
+  return ITSD_OK;
+}
+
+int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds, double* ms,
+                     double* flops, int* shapes, int* n_ops, void* stream) {
+  if (!u || !x || !t || !n_ops) return fail(ITSD_ERR_INVALID, "null argument");
+  if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_ops: DDPM only");
+  CHK(check_batch(u, n));
+  HIPCHK(hipSetDevice(u->device));
+  hipStream_t s = u->stream;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  float* eps = nullptr;
+  HIPCHK(hipMalloc(&eps, (size_t)n * 3 * u->H * u->H * 4));
+  CHK(temb_rows(u, t, n, 0, false, u->proj_buf, s));
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+  std::vector<int> kd;
+  std::vector<double> fl;
+  RunCtx c{};
+  c.nb = n; c.x = x; c.x_mod = n;
+  c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
+  c.label_mod = n; c.uncond_from = -1;
+  c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
+  c.census = true; c.evs = &evs; c.ev_kind = &kd; c.ev_flops = &fl;
+  int r = run_program(u, c, s);
+  hipError_t e = hipStreamSynchronize(s);
+  // launch order: head, ops..., tail GN, tail
+  int k = 0;
+  for (size_t i = 0; i < evs.size(); ++i) {
+    float m = 0.f;
+    if (r == ITSD_OK && e == hipSuccess) hipEventElapsedTime(&m, evs[i].first, evs[i].second);
+    hipEventDestroy(evs[i].first);
+    hipEventDestroy(evs[i].second);
+    if (k >= max_ops) continue;
+    if (kinds) kinds[k] = kd[i];
+    if (ms) ms[k] = m;
+    if (flops) flops[k] = fl[i];
+    if (shapes) {
+      int* sh = shapes + 6 * k;
+      for (int q = 0; q < 6; ++q) sh[q] = 0;
+      if (i >= 1 && i - 1 < u->ops.size()) {
+        const Op& o = u->ops[i - 1];
+        const Act& out = u->acts[o.dst];
+        const Act& in = u->acts[o.src1];
+        sh[0] = n * out.H * out.W;
+        sh[1] = o.kind == OP_CONV ? o.Cout : out.C;
+        sh[2] = o.kind == OP_CONV ? o.K : in.C + (o.src2 >= 0 ? u->acts[o.src2].C : 0);
+        sh[3] = out.H;
+        sh[4] = o.ksize;
+        sh[5] = o.stride * 10 + o.upsample;
+      }
+    }
+    ++k;
+  }
+  *n_ops = k;
+  hipFree(eps);
+  CHK(r);
+  HIPCHK(e);
   return ITSD_OK;
 }
 

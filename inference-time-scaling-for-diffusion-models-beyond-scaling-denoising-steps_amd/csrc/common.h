@@ -75,6 +75,7 @@ struct ConvArgs {
   void* out;                         // [M][Cout]
   int M;                             // n * Hout * Wout
   float* stats;                      // channel-statistics slab [slot][2][Cout] for the consumer GN, or null
+  const void* zero;                  // >= 16 zero bytes: DMA source for padded / out-of-range rows
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

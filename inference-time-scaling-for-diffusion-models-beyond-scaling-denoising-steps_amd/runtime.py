@@ -60,6 +60,9 @@ _SIGS = {
     "itsd_profile_forward": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double), ctypes.c_void_p],
+    "itsd_profile_ops": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
     "itsd_last_error": [],
     "itsd_version": [],
 }
@@ -172,6 +175,23 @@ class NativeUNet:
         check(lib().itsd_profile_forward(self.h, x.data_ptr(), t.data_ptr(), x.shape[0], ctypes.byref(cm),
                                          ctypes.byref(cf), ctypes.byref(cl), ctypes.byref(tm), stream_ptr(x.device)))
         return {"conv_ms": cm.value, "conv_flops": cf.value, "conv_launches": cl.value, "total_ms": tm.value}
+
+    def profile_ops(self, x: torch.Tensor, t: torch.Tensor, max_ops: int = 512):
+        import numpy as np
+
+        kinds = np.zeros(max_ops, np.int32)
+        ms = np.zeros(max_ops, np.float64)
+        fl = np.zeros(max_ops, np.float64)
+        sh = np.zeros((max_ops, 6), np.int32)
+        n = ctypes.c_int()
+        check(lib().itsd_profile_ops(self.h, x.data_ptr(), t.data_ptr(), x.shape[0], max_ops,
+                                     kinds.ctypes.data, ms.ctypes.data, fl.ctypes.data, sh.ctypes.data,
+                                     ctypes.byref(n), stream_ptr(x.device)))
+        k = n.value
+        names = {0: "gn", 1: "conv", 2: "attn", -1: "head", -2: "tail"}
+        return [{"kind": names.get(int(kinds[i]), str(kinds[i])), "ms": float(ms[i]), "flops": float(fl[i]),
+                 "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
+                 "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5])} for i in range(k)]
 
 
 def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset: int = 0,

@@ -1,0 +1,56 @@
+"""Per-launch census of one UNet forward on the GPU (HIP events around every launch).
+
+    python tools/census.py [--n 256] [--precision bf16] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+import itsd
+from itsd.arch import ARCH_A
+from itsd.model import UNet
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    a = ARCH_A
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=args.precision, weights="gauss")
+    net.to("cuda:0")
+    nat = net.native(args.n)
+    x = torch.randn(args.n, 3, 32, 32, device="cuda")
+    t = torch.full((args.n,), 500, dtype=torch.int32, device="cuda")
+    for _ in range(args.reps):
+        ops = nat.profile_ops(x, t)
+    tot = sum(o["ms"] for o in ops)
+    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    print(f"{'#':>3} {'kind':5} {'M':>7} {'N':>5} {'K':>5} {'H':>3} {'ks':>2} {'s/u':>3} {'ms':>8} {'TF/s':>7}")
+    for i, o in enumerate(ops):
+        tf = o["flops"] / (o["ms"] * 1e-3) / 1e12 if o["ms"] > 0 and o["flops"] > 0 else 0.0
+        print(f"{i:3d} {o['kind']:5} {o['M']:7d} {o['N']:5d} {o['K']:5d} {o['H']:3d} {o['ks']:2d} {o['stride_up']:3d} "
+              f"{o['ms']:8.4f} {tf:7.1f}")
+        key = o["kind"] if o["kind"] != "conv" else f"conv H{o['H']}"
+        agg[key][0] += 1
+        agg[key][1] += o["ms"]
+        agg[key][2] += o["flops"]
+    print(f"total {tot:.3f} ms")
+    for k, (c, m, f) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {k:10} launches {c:3d}  {m:8.3f} ms ({100 * m / tot:5.1f}%)  "
+              f"{(f / (m * 1e-3) / 1e12) if f else 0:7.1f} TF/s")
+    if args.json:
+        with open(args.json, "w") as fh:
+            json.dump(ops, fh)
+
+
+if __name__ == "__main__":
+    main()
