@@ -92,6 +92,7 @@ struct Op {
   int resid = -1;
   // ATTN
   int S = 0, C = 0;
+  int vt = -1, vt_from = 0;  // channel-major V buffer (conv: couts >= vt_from go there; attn: reads it)
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -295,10 +296,18 @@ struct Builder {
                                 get(a + ".proj_v.bias", out_ch)}, out_ch);
       int qkv = act(H, W, 3 * out_ch);
       conv(ga, -1, qkv, wqkv, bqkv, 3 * out_ch, 1, 1, 0, 0);
+      // MFMA attention (bf16): V goes channel-major to its own buffer from the conv epilogue
+      const int S = H * W;
+      int vt = -1;
+      if (u->bf16 && S <= 256 && S % 16 == 0 && out_ch % 64 == 0) {
+        vt = act(out_ch, S, 1);
+        u->ops.back().vt = vt;
+        u->ops.back().vt_from = 2 * out_ch;
+      }
       int ao = act(H, W, out_ch);
       Op at;
       at.kind = OP_ATTN;
-      at.src1 = qkv; at.dst = ao; at.S = H * W; at.C = out_ch;
+      at.src1 = qkv; at.dst = ao; at.S = H * W; at.C = out_ch; at.vt = vt;
       u->ops.push_back(at);
       o = conv_layer(ao, -1, a + ".proj", out_ch, 1, 1, 0, 0, H, W, -1, o);
     }
@@ -532,6 +541,11 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.M = c.nb * out.H * out.W;
     a.stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.zero = u->zero_page;
+    if (o.vt >= 0) {
+      if (o.vt_from % 128 || (out.H * out.W) % 8) return fail(ITSD_ERR_INVALID, "internal: bad channel-major V split");
+      a.vt_out = u->ap(o.vt);
+      a.vt_from = o.vt_from;
+    }
     a.zins = o.zins;
     {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
       const int epc = u->bf16 ? 8 : 4;
@@ -542,6 +556,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
   } else {
     AttnArgs a{};
     a.qkv = u->ap(o.src1);
+    a.vt = o.vt >= 0 ? u->ap(o.vt) : nullptr;
     a.out = u->ap(o.dst);
     a.S = o.S; a.C = o.C;
     a.scale = (float)std::pow((double)o.C, -0.5);

@@ -76,6 +76,8 @@ struct ConvArgs {
   int M;                             // n * Hout * Wout
   float* stats;                      // channel-statistics slab [slot][2][Cout] for the consumer GN, or null
   const void* zero;                  // >= 16 zero bytes: DMA source for padded / out-of-range rows
+  void* vt_out;                      // couts >= vt_from go channel-major to vt_out[img][co-vt_from][HWo]
+  int vt_from;                       // (the V of a fused q|k|v projection, for the MFMA attention)
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of
@@ -94,7 +96,8 @@ struct GNArgs {
 };
 
 struct AttnArgs {
-  const void* qkv;  // [n][S][3C]
+  const void* qkv;  // [n][S][3C]  (q | k | v per token; v unused when vt != null)
+  const void* vt;   // [n][C][S]   channel-major v (MFMA path) or null
   void* out;        // [n][S][C]
   int S, C;
   float scale;

@@ -106,6 +106,24 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
         *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
       }
   __syncthreads();
+  if (a.vt_out && tileC >= a.vt_from) {
+    // channel-major store of this (whole-V) tile: vt[img][c][pixel], 16-B chunks of
+    // consecutive pixels of one image (host: HWo % EPC == 0, vt_from % 128 == 0); + bias only.
+    const int Cv = a.Cout - a.vt_from;
+    for (int it = tid; it < 128 * (128 / EPC); it += 256) {
+      const int cl = it / (128 / EPC), pl = (it - cl * (128 / EPC)) * EPC;
+      const int co = tileC + cl, p = tileP + pl;
+      if (co >= a.Cout || p >= a.M) continue;
+      const int img = p / HWo, pi = p - img * HWo;
+      const float bb = a.bias[co];
+      u32x4 w;
+      T* we = (T*)&w;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(E[(pl + e) * EROW + cl] + bb);
+      *(u32x4*)((T*)a.vt_out + ((size_t)img * Cv + (co - a.vt_from)) * HWo + pi) = w;
+    }
+    return;
+  }
   const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
   constexpr int CPR = 128 / EPC;  // 16-B output chunks per tile row
   for (int it = tid; it < 128 * CPR; it += 256) {

@@ -175,8 +175,115 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   }
 }
 
+// MFMA attention (bf16 throughput path, S <= 256, S % 16 == 0, C % 32 == 0).
+// One block per (64-query chunk, image), 4 waves:
+//  1. scores = q k^T * C^-0.5 on v_mfma_f32_32x32x16_bf16, q and k rows read straight
+//     from the q|k|v projection (both operands are contiguous 16-B fragments);
+//  2. row softmax in fp32 over LDS, P rounded to bf16 in LDS;
+//  3. O^T = V^T P^T on MFMA with V^T channel-major (written so by the qkv conv epilogue)
+//     -> 4 consecutive channels per lane per store.
+constexpr int ATT_AQ = 64;
+__global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char asm_[];
+  const int S = a.S, C = a.C, C3 = 3 * a.C;
+  const int Sp = (S + 31) & ~31;
+  const int SROW = Sp + 4;            // fp32 score row
+  const int PROW = Sp * 2 + 16;       // bf16 P row (bytes), odd 16-B slot stride
+  float* Sc = (float*)asm_;
+  char* Pm = asm_ + 64 * SROW * 4;
+  const int img = blockIdx.y, q0 = blockIdx.x * ATT_AQ;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  {
+    const int qi = wid >> 1;
+    const int q = q0 + qi * 32 + rl;
+    const bool qv = q < S;
+    const bf16_t* qp = base + (size_t)(qv ? q : 0) * C3 + 8 * hh;
+    for (int kj = (wid & 1); kj < Sp / 32; kj += 2) {
+      const int key = kj * 32 + rl;
+      const bool kv = key < S;
+      const bf16_t* kp = base + (size_t)(kv ? key : 0) * C3 + C + 8 * hh;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      for (int c = 0; c < C; c += 16) {
+        const bf16x8 af = qv ? *(const bf16x8*)(qp + c) : z8;
+        const bf16x8 bk = kv ? *(const bf16x8*)(kp + c) : z8;
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = qi * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        Sc[row * SROW + kj * 32 + rl] = kv ? acc[r] * a.scale : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  for (int r = wid * 16; r < wid * 16 + 16; ++r) {
+    float m = -INFINITY;
+    for (int j = lane; j < Sp; j += 64) m = fmaxf(m, Sc[r * SROW + j]);
+    m = wave_max(m);
+    float sum = 0.f;
+    for (int j = lane; j < Sp; j += 64) {
+      const float e = expf(Sc[r * SROW + j] - m);
+      Sc[r * SROW + j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+    for (int j = lane; j < Sp; j += 64) ((bf16_t*)(Pm + r * PROW))[j] = f2bf(Sc[r * SROW + j] * inv);
+  }
+  __syncthreads();
+  const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
+  bf16_t* out = (bf16_t*)a.out + (size_t)img * S * C;
+  for (int t = wid; t < 2 * (C / 32); t += 4) {
+    const int ci = t >> 1, qi = t & 1;
+    const bf16_t* vp = vt + (size_t)(ci * 32 + rl) * S + 8 * hh;
+    const char* pp = Pm + (qi * 32 + rl) * PROW + 16 * hh;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int k = 0; k < Sp; k += 16) {
+      const bf16x8 av = (k + 8 * hh < S) ? *(const bf16x8*)(vp + k) : z8;
+      const bf16x8 bp = *(const bf16x8*)(pp + 2 * k);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bp, acc, 0, 0, 0);
+    }
+    const int q = q0 + qi * 32 + rl;
+    if (q < S) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = ci * 32 + 8 * g + 4 * hh;
+        uint2 w2;
+        w2.x = (uint32_t)f2bf(acc[4 * g]) | ((uint32_t)f2bf(acc[4 * g + 1]) << 16);
+        w2.y = (uint32_t)f2bf(acc[4 * g + 2]) | ((uint32_t)f2bf(acc[4 * g + 3]) << 16);
+        *(uint2*)(out + (size_t)q * C + c) = w2;
+      }
+    }
+  }
+}
+
+size_t attn_mfma_smem(int S) {
+  const int Sp = (S + 31) & ~31;
+  return (size_t)64 * (Sp + 4) * 4 + (size_t)64 * (Sp * 2 + 16);
+}
+
 template <typename T>
 hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (a.vt) {
+      static bool attr = false;
+      const size_t sm = attn_mfma_smem(a.S);
+      if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)attn_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)attn_mfma_smem(256));
+        if (e != hipSuccess) return e;
+        attr = true;
+      }
+      hipLaunchKernelGGL(attn_mfma_kernel, dim3((a.S + ATT_AQ - 1) / ATT_AQ, n), dim3(256), sm, s, a);
+      return hipGetLastError();
+    }
+  }
   const int qc = att_qc(a.S);
   dim3 grid((a.S + qc - 1) / qc, n);
   hipLaunchKernelGGL(attn_kernel<T>, grid, dim3(256), qc * a.S * sizeof(float), s, a);
@@ -187,15 +294,21 @@ template hipError_t launch_attn<bf16_t>(const AttnArgs&, int, hipStream_t);
 
 // ============================================================================ head conv
 // head = Conv2d(3, ch, 3, padding=1) (Model.py:219) from the NCHW fp32 sampler state
-// to NHWC activations. One thread per (pixel, 4 output channels).
+// to NHWC activations. One thread per (pixel, 16-B chunk of output channels);
+// consecutive threads cover one pixel's channel row (coalesced stores), weights in LDS.
 template <typename T>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  extern __shared__ float hw[];  // [Cout][27] then bias [Cout]
+  for (int i = threadIdx.x; i < a.Cout * 27; i += 256) hw[i] = a.w[i];
+  for (int i = threadIdx.x; i < a.Cout; i += 256) hw[a.Cout * 27 + i] = a.b[i];
+  __syncthreads();
   const int HW = a.H * a.W;
-  const int cq = a.Cout / 4;
+  const int cq = a.Cout / EPC;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long total = (long long)a.n * HW * cq;
   if (idx >= total) return;
-  const int c4 = (int)(idx % cq);
+  const int c0 = (int)(idx % cq) * EPC;
   const long long pix = idx / cq;
   const int img = (int)(pix / HW);
   const int rem = (int)(pix - (long long)img * HW);
@@ -211,25 +324,25 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
         const int iy = y + ky - 1, ix = x + kx - 1;
         in[ci * 9 + ky * 3 + kx] = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? xs[ci * HW + iy * a.W + ix] : 0.0f;
       }
-  float o[4];
+  u32x4 w;
+  T* we = (T*)&w;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int co = c4 * 4 + e;
-    const float* w = a.w + co * 27;
+  for (int e = 0; e < EPC; ++e) {
+    const float* wr = hw + (c0 + e) * 27;
     float acc = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc = fmaf(w[k], in[k], acc);
-    o[e] = acc + a.b[co];
+    for (int k = 0; k < 27; ++k) acc = fmaf(wr[k], in[k], acc);
+    we[e] = Elem<T>::to(acc + hw[a.Cout * 27 + c0 + e]);
   }
-  T* out = (T*)a.out + (size_t)pix * a.Cout + c4 * 4;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) out[e] = Elem<T>::to(o[e]);
+  *(u32x4*)((T*)a.out + (size_t)pix * a.Cout + c0) = w;
 }
 
 template <typename T>
 hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
-  const long long total = (long long)a.n * a.H * a.W * (a.Cout / 4);
-  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const long long total = (long long)a.n * a.H * a.W * (a.Cout / EPC);
+  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), a.Cout * 28 * sizeof(float), s,
+                     a);
   return hipGetLastError();
 }
 template hipError_t launch_head<float>(const HeadArgs&, hipStream_t);
@@ -344,8 +457,116 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
   }
 }
 
+// Tiled tail: one block per 64 output pixels (64/W full rows of one image); the input
+// halo rows are staged once in LDS (coalesced 16-B loads, padded pixel stride: no bank
+// conflicts) and 4 threads per pixel split the channels, reduced by lane shuffles.
+template <typename T>
+__global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int C = a.C, W = a.W, H = a.H;
+  const int rpb = 64 / W;
+  const int HW = H * W;
+  const int PST = C * (int)sizeof(T) + 16;
+  float* wl = (float*)tsm;           // [9][C][3]
+  char* halo = tsm + 27 * C * 4;     // [(rpb+2)*(W+2)] pixels of PST bytes
+  for (int i = threadIdx.x; i < 27 * C; i += 256) {
+    const int co = i / (C * 9);
+    const int r = i - co * C * 9;
+    const int ci = r / 9, tap = r - ci * 9;
+    wl[(tap * C + ci) * 3 + co] = a.w[i];
+  }
+  const int bpi = H / rpb;
+  const int img = blockIdx.x / bpi, y0 = (blockIdx.x % bpi) * rpb;
+  const int tid = threadIdx.x, pl = tid >> 2, cq = tid & 3;
+  const int py = pl / W, px = pl - (pl / W) * W;
+  const int cpq = C / 4;
+  float eps[3] = {0.f, 0.f, 0.f}, unc[3] = {0.f, 0.f, 0.f};
+  for (int pass = 0; pass < (a.cfg ? 2 : 1); ++pass) {
+    const int im = img + pass * a.n;
+    __syncthreads();
+    const T* gb = (const T*)a.g + (size_t)im * HW * C;
+    const int cpp = C / EPC, npx = (rpb + 2) * (W + 2);
+    for (int i = tid; i < npx * cpp; i += 256) {
+      const int hp = i / cpp, ch = i - hp * cpp;
+      const int hy = hp / (W + 2), hx = hp - hy * (W + 2);
+      const int gy = y0 - 1 + hy, gx = hx - 1;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = *(const u32x4*)(gb + ((size_t)gy * W + gx) * C + ch * EPC);
+      *(u32x4*)(halo + hp * PST + ch * 16) = v;
+    }
+    __syncthreads();
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        const char* hpix = halo + ((py + ky) * (W + 2) + px + kx) * PST;
+        const float* wp = wl + (ky * 3 + kx) * C * 3;
+        for (int c = cq * cpq; c < (cq + 1) * cpq; c += EPC) {
+          const u32x4 v = *(const u32x4*)(hpix + c * (int)sizeof(T));
+          const T* ve = (const T*)&v;
+#pragma unroll
+          for (int e = 0; e < EPC; ++e) {
+            const float gv = Elem<T>::tof(ve[e]);
+            s0 = fmaf(gv, wp[(c + e) * 3 + 0], s0);
+            s1 = fmaf(gv, wp[(c + e) * 3 + 1], s1);
+            s2 = fmaf(gv, wp[(c + e) * 3 + 2], s2);
+          }
+        }
+      }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    float* dst = pass ? unc : eps;
+    dst[0] = s0 + a.b[0]; dst[1] = s1 + a.b[1]; dst[2] = s2 + a.b[2];
+  }
+  if (cq >= 3) return;
+  float e = cq == 0 ? eps[0] : (cq == 1 ? eps[1] : eps[2]);
+  if (a.cfg) {
+#pragma clang fp contract(off)
+    const float u = cq == 0 ? unc[0] : (cq == 1 ? unc[1] : unc[2]);
+    e = a.guide_w1 * e - a.guide_w * u;
+  }
+  const int rem = (y0 + py) * W + px;
+  const size_t o = ((size_t)img * 3 + cq) * HW + rem;
+  if (!a.step_mode) {
+    a.eps_out[o] = e;
+    return;
+  }
+  {
+#pragma clang fp contract(off)
+    const int t = *a.tsel;
+    const float xv = a.x[o];
+    const float mean = a.coeff1[t] * xv - a.coeff2[t] * e;
+    float xn = mean;
+    if (t > 0) {
+      const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o]
+                              : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+      xn = mean + a.sqrt_var[t] * z;
+    }
+    if (xn != xn) atomicOr(a.nan_flag, 1);
+    if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+    a.x[o] = xn;
+  }
+}
+
 template <typename T>
 hipError_t launch_tail(const TailArgs& a, hipStream_t s) {
+  if (a.W <= 64 && 64 % a.W == 0 && a.H % (64 / a.W) == 0 && a.C % 32 == 0) {
+    const size_t sm = 27 * a.C * 4 + (size_t)(64 / a.W + 2) * (a.W + 2) * (a.C * sizeof(T) + 16);
+    if (sm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute((const void*)tail2_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(tail2_kernel<T>, dim3(a.n * (a.H / (64 / a.W))), dim3(256), sm, s, a);
+    return hipGetLastError();
+  }
   const long long total = (long long)a.n * a.H * a.W;
   hipLaunchKernelGGL(tail_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 27 * a.C * sizeof(float), s, a);
   return hipGetLastError();
