@@ -128,6 +128,10 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
                      double* ms, double* flops, int* shapes, int* n_ops, void* stream);
 
+/* Process-wide tuning switches for A/B measurements. Keys: "conv_variant"
+ * (0 = default: DMA-ring conv, 4 stages; 1 = register-staged; 2/3 = DMA ring, 2/3 stages). */
+int itsd_set_option(const char* key, int value);
+
 const char* itsd_last_error(void);
 int itsd_version(void);
 

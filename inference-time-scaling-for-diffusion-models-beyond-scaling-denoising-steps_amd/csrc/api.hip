@@ -678,6 +678,16 @@ extern "C" {
 
 int itsd_version(void) { return 1; }
 
+int itsd_set_option(const char* key, int value) {
+  if (!key) return fail(ITSD_ERR_INVALID, "null key");
+  if (!std::strcmp(key, "conv_variant")) {
+    if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "conv_variant in [0,3]");
+    itsd::g_conv_variant = value;
+    return ITSD_OK;
+  }
+  return fail(ITSD_ERR_INVALID, std::string("unknown option ") + key);
+}
+
 const char* itsd_last_error(void) { return g_err.c_str(); }
 
 int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights, int n_weights, int device,

@@ -6,6 +6,8 @@
 
 namespace itsd {
 
+extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_set_option)
+
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;

@@ -32,10 +32,9 @@ constexpr int CONV_BN = 128;  // pixels per block
 constexpr int ROWB = 128;     // bytes per LDS row
 constexpr int TILEB = 128 * ROWB;
 constexpr int EROW = 132;  // epilogue LDS row (floats)
-constexpr int EPI_BYTES = 128 * EROW * 4;
+constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + statistics partials
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
-constexpr int PIPE_NS = 4;  // LDS ring depth of conv_pipe
-constexpr int PIPE_SMEM = PIPE_NS * 2 * TILEB;
+int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -185,19 +184,54 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     __syncthreads();
     const int Gt = stat_slot_px(HWo);  // host guarantees 128 % HWo == 0 or HWo % 128 == 0
     const int S = 128 / Gt;
-    for (int item = tid; item < S * 128; item += 256) {
-      const int s = item >> 7, cl = item & 127;
-      const int co = tileC + cl, p0 = tileP + s * Gt;
-      if (co >= a.Cout || p0 >= a.M) continue;
-      float sum = 0.f, sq = 0.f;
-      for (int k = 0; k < Gt; ++k) {
-        const float v = E[(s * Gt + k) * EROW + cl];
-        sum += v;
-        sq = fmaf(v, v, sq);
+    if (Gt >= 16) {
+      // pass 1: 8 groups of 16 pixel rows x 32 channel quads, 16-B LDS reads
+      float* R = E + 128 * EROW;  // [8 groups][2][128]
+      {
+        const int cq = tid & 31, pg = tid >> 5;
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < 16; ++k) {
+          const int pl = pg * 16 + k;
+          if (tileP + pl < a.M) {
+            const f32x4 v = *(const f32x4*)(E + pl * EROW + 4 * cq);
+            s4 += v;
+            q4 += v * v;
+          }
+        }
+        *(f32x4*)(R + (pg * 2) * 128 + 4 * cq) = s4;
+        *(f32x4*)(R + (pg * 2 + 1) * 128 + 4 * cq) = q4;
       }
-      const long long slot = p0 / Gt;
-      a.stats[(slot * 2) * a.Cout + co] = sum;
-      a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
+      __syncthreads();
+      // pass 2: groups -> slots in fixed order (deterministic)
+      const int gps = Gt / 16;
+      for (int item = tid; item < S * 128; item += 256) {
+        const int s = item >> 7, cl = item & 127;
+        const int co = tileC + cl, p0 = tileP + s * Gt;
+        if (co >= a.Cout || p0 >= a.M) continue;
+        float sum = 0.f, sq = 0.f;
+        for (int g = s * gps; g < (s + 1) * gps; ++g) {
+          sum += R[(g * 2) * 128 + cl];
+          sq += R[(g * 2 + 1) * 128 + cl];
+        }
+        const long long slot = p0 / Gt;
+        a.stats[(slot * 2) * a.Cout + co] = sum;
+        a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
+      }
+    } else {
+      for (int item = tid; item < S * 128; item += 256) {
+        const int s = item >> 7, cl = item & 127;
+        const int co = tileC + cl, p0 = tileP + s * Gt;
+        if (co >= a.Cout || p0 >= a.M) continue;
+        float sum = 0.f, sq = 0.f;
+        for (int k = 0; k < Gt; ++k) {
+          const float v = E[(s * Gt + k) * EROW + cl];
+          sum += v;
+          sq = fmaf(v, v, sq);
+        }
+        const long long slot = p0 / Gt;
+        a.stats[(slot * 2) * a.Cout + co] = sum;
+        a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
+      }
     }
   }
 }
@@ -217,13 +251,12 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T>
-__global__ __launch_bounds__(256, 1) void conv_pipe(ConvArgs a) {
+template <typename T, int NS, bool LIN>
+__global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int BK = 8 * EPC;
   constexpr int STAGE = 2 * TILEB;
-  constexpr int NS = PIPE_NS;
-  __shared__ __attribute__((aligned(16))) char smem[PIPE_SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[(NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
@@ -239,24 +272,49 @@ __global__ __launch_bounds__(256, 1) void conv_pipe(ConvArgs a) {
   // This lane's DMA rows: instruction q of wave w fills rows 8*(4w+q) .. +7 (1 KiB);
   // lane L lands at row 8*(4w+q) + L/8, slot L%8, so it must fetch logical chunk
   // (L%8) ^ ((row>>1)&7) (the read-side swizzle applied to the source).
+  // Per-lane gather state, computed once: the weight row pointer, and for the pixel
+  // row a bitmask of the taps that land inside the (virtual) input plus, per tap, a
+  // 32-bit element offset = pixel term (per lane) + tap term (per stage, scalar).
+  // Nearest-x2 upsample / zero-insertion make the pixel term tap-dependent, so those
+  // layers keep a per-tap row/column table instead (rowt/colt: -1 = padding).
   const T* arow[4];
-  int bimg[4], biy[4], bix[4], bch[4];
-  bool bval[4];
+  int pix1[4], pix2[4];  // element offset of (iy0, ix0) in src1 / src2, + chunk
+  unsigned tmask[4];
+  int rowt[4][5], colt[4][5], chk[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = 8 * (4 * wid + q) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int co = tileC + r;
-    arow[q] = co < a.Cout ? (const T*)a.wt + (size_t)co * a.K + c * EPC : nullptr;
+    arow[q] = (const T*)a.wt + (size_t)(co < a.Cout ? co : 0) * a.K + c * EPC;
+    if (co >= a.Cout) arow[q] = nullptr;
     const int p = tileP + r;
-    bval[q] = p < a.M;
+    const bool pv = p < a.M;
     const int img = p / HWo;
     const int rem = p - img * HWo;
     const int oy = rem / a.Wout;
-    bimg[q] = img;
-    biy[q] = oy * a.stride - a.pad;
-    bix[q] = (rem - oy * a.Wout) * a.stride - a.pad;
-    bch[q] = c * EPC;
+    const int iy0 = oy * a.stride - a.pad;
+    const int ix0 = (rem - oy * a.Wout) * a.stride - a.pad;
+    const int pl = (img * a.Hin + iy0) * a.Win + ix0;
+    pix1[q] = pl * a.C1 + c * EPC;
+    pix2[q] = pl * a.C2 + c * EPC;
+    unsigned m = 0;
+    for (int ky = 0; ky < a.ksize; ++ky)
+      for (int kx = 0; kx < a.ksize; ++kx) {
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        bool ok = pv && iy >= 0 && iy < Hv && ix >= 0 && ix < Wv;
+        if (a.zins) ok = ok && !((iy | ix) & 1);
+        if (ok) m |= 1u << (ky * a.ksize + kx);
+      }
+    tmask[q] = m;
+    chk[q] = c * EPC;
+    if constexpr (!LIN) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        rowt[q][k] = (img * a.Hin + ((iy0 + k) >> 1)) * a.Win;
+        colt[q][k] = (ix0 + k) >> 1;
+      }
+    }
   }
 
   auto issue = [&](int kc) {
@@ -265,10 +323,11 @@ __global__ __launch_bounds__(256, 1) void conv_pipe(ConvArgs a) {
     const int ky = tap / a.ksize, kx = tap - (tap / a.ksize) * a.ksize;
     char* sA = smem + (kc % NS) * STAGE;
     char* sB = sA + TILEB;
-    const T* src;
-    int Cs, cs0;
-    if (ci0 < a.C1) { src = (const T*)a.src1; Cs = a.C1; cs0 = ci0; }
-    else { src = (const T*)a.src2; Cs = a.C2; cs0 = ci0 - a.C1; }
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int Cs = s1 ? a.C1 : a.C2;
+    const int cs0 = s1 ? ci0 : ci0 - a.C1;
+    const int toff = (ky * a.Win + kx) * Cs + cs0;  // scalar tap term
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const T* ga = arow[q] ? arow[q] + (size_t)kc * BK : zero;
@@ -276,11 +335,10 @@ __global__ __launch_bounds__(256, 1) void conv_pipe(ConvArgs a) {
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      int iy = biy[q] + ky, ix = bix[q] + kx;
-      bool ok = bval[q] && iy >= 0 && iy < Hv && ix >= 0 && ix < Wv;
-      if (a.zins) ok = ok && !((iy | ix) & 1);
-      if (a.upsample | a.zins) { iy >>= 1; ix >>= 1; }
-      const T* gb = ok ? src + (((size_t)bimg[q] * a.Hin + iy) * a.Win + ix) * Cs + cs0 + bch[q] : zero;
+      int off;
+      if constexpr (LIN) off = (s1 ? pix1[q] : pix2[q]) + toff;
+      else off = (rowt[q][ky] + colt[q][kx]) * Cs + cs0 + chk[q];
+      const T* gb = ((tmask[q] >> tap) & 1u) ? src + off : zero;
       __builtin_amdgcn_global_load_lds((const void*)gb, (lds_ptr_t)(sB + (4 * wid + q) * 1024), 16, 0, 0);
     }
   };
@@ -404,8 +462,13 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
   const int Cin = a.C1 + a.C2;
   const bool pipe = a.zero && Cin % BK == 0 && a.C1 % BK == 0 && a.K == a.ksize * a.ksize * Cin;
-  if (pipe) hipLaunchKernelGGL(conv_pipe<T>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
+  const int v = g_conv_variant;
+  const bool lin = !(a.upsample | a.zins);
+  if (!pipe || v == 1) hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
+  else if (v == 2 && lin) hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+  else if (v == 2) hipLaunchKernelGGL((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
+  else if (v == 3) hipLaunchKernelGGL((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ _SIGS = {
     "itsd_profile_ops": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
+    "itsd_set_option": [ctypes.c_char_p, ctypes.c_int],
     "itsd_last_error": [],
     "itsd_version": [],
 }
@@ -201,6 +202,10 @@ def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset
                            int(seed) & ((1 << 64) - 1), int(stream_id) & 0xFFFFFFFF, int(cand_offset),
                            stream_ptr(out.device)))
     return out
+
+
+def set_option(key: str, value: int) -> None:
+    check(lib().itsd_set_option(key.encode(), int(value)))
 
 
 def verify(kind: int, images: torch.Tensor, n_cand: int) -> torch.Tensor:

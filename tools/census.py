@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
     args = ap.parse_args()
     a = ARCH_A
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=args.precision, weights="gauss")
@@ -30,6 +31,20 @@ def main():
     nat = net.native(args.n)
     x = torch.randn(args.n, 3, 32, 32, device="cuda")
     t = torch.full((args.n,), 500, dtype=torch.int32, device="cuda")
+    if args.variants:
+        from itsd import runtime as rt
+        for rnd in range(3):
+            for v in [int(q) for q in args.variants.split(",")]:
+                rt.set_option("conv_variant", v)
+                ops = nat.profile_ops(x, t)
+                conv = [o for o in ops if o["kind"] == "conv"]
+                by = defaultdict(lambda: [0.0, 0.0])
+                for o in conv:
+                    by[o["H"]][0] += o["ms"]
+                    by[o["H"]][1] += o["flops"]
+                print(f"round {rnd} variant {v}: conv {sum(o['ms'] for o in conv):.3f} ms total {sum(o['ms'] for o in ops):.3f} ms | "
+                      + " ".join(f"H{h}:{m:.3f}ms/{f / m / 1e9:.0f}TF" for h, (m, f) in sorted(by.items())))
+        rt.set_option("conv_variant", 0)
     for _ in range(args.reps):
         ops = nat.profile_ops(x, t)
     tot = sum(o["ms"] for o in ops)
