@@ -152,6 +152,10 @@ struct itsd_unet {
   int* d_t = nullptr;
   int* d_nan = nullptr;
   void* zero_page = nullptr;  // 1 KiB of zeros (conv DMA source for padding)
+  float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
+  int* splitk_cnt = nullptr;   // per-tile tickets, zeroed once; each launch's last arriver resets its own
+  static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
+  static constexpr int kSplitkTiles = 65536;
 
   hipStream_t stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -541,6 +545,10 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.M = c.nb * out.H * out.W;
     a.stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.zero = u->zero_page;
+    a.splitk_ws = u->splitk_ws;
+    a.splitk_cnt = u->splitk_cnt;
+    a.splitk_cap = itsd_unet::kSplitkCap;
+    a.splitk_tiles = itsd_unet::kSplitkTiles;
     if (o.vt >= 0) {
       if (o.vt_from % 128 || (out.H * out.W) % 8) return fail(ITSD_ERR_INVALID, "internal: bad channel-major V split");
       a.vt_out = u->ap(o.vt);
@@ -685,6 +693,10 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_conv_variant = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "splitk")) {
+    itsd::g_splitk = value ? 1 : 0;
+    return ITSD_OK;
+  }
   return fail(ITSD_ERR_INVALID, std::string("unknown option ") + key);
 }
 
@@ -718,6 +730,9 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipMalloc(&u->d_nan, 64));
   HIPCHK(hipMalloc(&u->zero_page, 1024));
   HIPCHK(hipMemset(u->zero_page, 0, 1024));
+  HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
+  HIPCHK(hipMalloc(&u->splitk_cnt, itsd_unet::kSplitkTiles * 4));
+  HIPCHK(hipMemset(u->splitk_cnt, 0, itsd_unet::kSplitkTiles * 4));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -736,6 +751,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   hipFree(u->wdev); hipFree(u->ws); hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
   hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
   hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->zero_page);
+  hipFree(u->splitk_ws); hipFree(u->splitk_cnt);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
   if (u->ev_out) hipEventDestroy(u->ev_out);

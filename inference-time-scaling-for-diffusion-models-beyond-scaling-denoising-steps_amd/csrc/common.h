@@ -7,6 +7,7 @@
 namespace itsd {
 
 extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_set_option)
+extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
 
@@ -80,6 +81,10 @@ struct ConvArgs {
   const void* zero;                  // >= 16 zero bytes: DMA source for padded / out-of-range rows
   void* vt_out;                      // couts >= vt_from go channel-major to vt_out[img][co-vt_from][HWo]
   int vt_from;                       // (the V of a fused q|k|v projection, for the MFMA attention)
+  float* splitk_ws;                  // split-K partial tiles (capacity splitk_cap floats) or null
+  int* splitk_cnt;                   // per-tile arrival tickets (zero between launches)
+  long long splitk_cap;
+  int splitk_tiles;                  // ticket capacity
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -23,6 +23,8 @@
 //  * conv_igemm (generic fallback): register-staged double buffer.
 // Epilogue (shared, LDS-staged): + bias + temb_proj row (+ CFG cond_proj row) +
 // residual, coalesced 16-B stores, and the consumer GroupNorm's channel statistics.
+#include <algorithm>
+
 #include "common.h"
 
 namespace itsd {
@@ -35,6 +37,7 @@ constexpr int EROW = 132;  // epilogue LDS row (floats)
 constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + statistics partials
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
+int g_splitk = 1;        // split-K for under-filled grids (variant 2)
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -245,6 +248,92 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[2][2]) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 }
 
+// ---------------------------------------------------------------------------- split-K
+// In-launch split-K combine (MI355X guide, "In-launch split-K reduction"): every slice
+// writes its fp32 partial tile (thread-native layout, 16-B stores), drains, and one
+// lane releases (agent scope) then takes a ticket; the block drawing S-1 acquires,
+// resets the ticket for the next launch, and sums all partials in slice order 0..S-1
+// (its own from registers) -- bit-identical whichever slice arrives last -- then runs
+// the fused epilogue. Correct for any placement of the slices over XCDs.
+struct TileId {
+  int x, y, z;
+};
+
+// Bijective XCD-aware remap (MI355X guide T1): the dispatcher deals linear block ids
+// round-robin over the 8 XCDs, so XCD (b % 8) is given the contiguous tile-id range
+// [start, start + count) of the cout-major order t = (z*gy + y)*gx + x. Blocks that
+// share a cout tile (its weights) then share one L2 -- at the 8x8 / 4x4 levels the
+// weight matrices (up to 9.4 MB) do not fit one 4 MB L2 if every XCD needs all of them.
+// Speed only: correctness never depends on placement.
+__device__ __forceinline__ TileId tile_of_block() {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int B = gx * gy * gz;
+  const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xcd = b & 7, q = B >> 3, r = B & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  TileId id;
+  id.x = t % gx;
+  id.y = (t / gx) % gy;
+  id.z = t / (gx * gy);
+  return id;
+}
+
+__device__ __forceinline__ bool splitk_reduce(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int z, int S,
+                                              const TileId& bt) {
+  const int tid = threadIdx.x;
+  const long long tile = (long long)bt.y * gridDim.x + bt.x;
+  float* slab = a.splitk_ws + (size_t)tile * S * 16384;
+  float* mine = slab + (size_t)z * 16384 + tid * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        *(f32x4*)(mine + (i * 2 + j) * 16 + 4 * g) = v;
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = (int*)smem;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(a.splitk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      a.splitk_cnt[tile] = 0;
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();
+  if (!last) return false;
+  f32x16 tot[2][2];
+  zero_acc(tot);
+  for (int zz = 0; zz < S; ++zz) {
+    const float* src = slab + (size_t)zz * 16384 + tid * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *(const f32x4*)(src + (i * 2 + j) * 16 + 4 * g);  // own slice too (same values)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tot[i][j][4 * g + e] += v[e];
+        }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
+  return true;
+}
+
 // ---------------------------------------------------------------------------- pipelined
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -260,7 +349,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
-  const int tileP = blockIdx.x * CONV_BN, tileC = blockIdx.y * CONV_BM;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * CONV_BN, tileC = bt.y * CONV_BM;
   const int Cin = a.C1 + a.C2;
   const int cpt = Cin / BK;  // K-chunks per tap
   const int nK = a.ksize * a.ksize * cpt;
@@ -345,22 +435,26 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
 
   f32x16 acc[2][2];
   zero_acc(acc);
+  // split-K: slice z of gridDim.z covers K-stages [k0, k1)
+  const int S = gridDim.z, z = bt.z;
+  const int k0 = (int)((long long)nK * z / S), k1 = (int)((long long)nK * (z + 1) / S);
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nK) issue(s);
-  for (int kc = 0; kc < nK; ++kc) {
+    if (k0 + s < k1) issue(k0 + s);
+  for (int kc = k0; kc < k1; ++kc) {
     // stage kc must have landed: keep the younger in-flight stages (8 DMA each) pending
-    const int ahead = min(NS - 2, nK - 1 - kc);
+    const int ahead = min(NS - 2, k1 - 1 - kc);
     if (ahead >= 2) wait_vmcnt<16>();
     else if (ahead == 1) wait_vmcnt<8>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    if (kc + NS - 1 < nK) issue(kc + NS - 1);
+    if (kc + NS - 1 < k1) issue(kc + NS - 1);
     const char* A = smem + (kc % NS) * STAGE;
     mma_stage<T>(A, A + TILEB, acc, wm, wn, rl, hh);
   }
   wait_vmcnt<0>();
   __syncthreads();
+  if (S > 1 && !splitk_reduce(a, acc, smem, z, S, bt)) return;
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
@@ -373,7 +467,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int tileP = blockIdx.x * CONV_BN, tileC = blockIdx.y * CONV_BM;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * CONV_BN, tileC = bt.y * CONV_BM;
   const int c16 = tid & 7, r0 = tid >> 3;
   const int Cin = a.C1 + a.C2;
   const int HWo = a.Hout * a.Wout;
@@ -464,6 +559,17 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   const bool pipe = a.zero && Cin % BK == 0 && a.C1 % BK == 0 && a.K == a.ksize * a.ksize * Cin;
   const int v = g_conv_variant;
   const bool lin = !(a.upsample | a.zins);
+  if (pipe && v == 2 && a.splitk_ws && g_splitk) {
+    // under-filled grids (the 8x8 / 4x4 levels): split K so that >= ~2 blocks per CU exist,
+    // keeping >= 8 K-stages per slice
+    const int blocks = (int)(grid.x * grid.y);
+    const int nK = a.ksize * a.ksize * (Cin / BK);
+    int S = 1;
+    if (blocks < 256) S = std::min((512 + blocks - 1) / blocks, nK / 8);  // measured: helps only < 1 block/CU
+    while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
+    if (blocks > a.splitk_tiles) S = 1;
+    grid.z = S < 1 ? 1 : S;
+  }
   if (!pipe || v == 1) hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
   else if (v == 2 && lin) hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
   else if (v == 2) hipLaunchKernelGGL((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);

@@ -34,8 +34,10 @@ def main():
     if args.variants:
         from itsd import runtime as rt
         for rnd in range(3):
-            for v in [int(q) for q in args.variants.split(",")]:
-                rt.set_option("conv_variant", v)
+            for v in args.variants.split(","):  # e.g. "2", "2s0" (variant 2, split-K off)
+                vv, _, sk = v.partition("s")
+                rt.set_option("conv_variant", int(vv))
+                rt.set_option("splitk", int(sk) if sk else 1)
                 ops = nat.profile_ops(x, t)
                 conv = [o for o in ops if o["kind"] == "conv"]
                 by = defaultdict(lambda: [0.0, 0.0])
@@ -44,7 +46,8 @@ def main():
                     by[o["H"]][1] += o["flops"]
                 print(f"round {rnd} variant {v}: conv {sum(o['ms'] for o in conv):.3f} ms total {sum(o['ms'] for o in ops):.3f} ms | "
                       + " ".join(f"H{h}:{m:.3f}ms/{f / m / 1e9:.0f}TF" for h, (m, f) in sorted(by.items())))
-        rt.set_option("conv_variant", 0)
+        rt.set_option("conv_variant", 2)
+        rt.set_option("splitk", 1)
     for _ in range(args.reps):
         ops = nat.profile_ops(x, t)
     tot = sum(o["ms"] for o in ops)
