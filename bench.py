@@ -133,7 +133,7 @@ def main():
         peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": "conv_igemm<bf16>" if args.precision == "bf16" else "conv_igemm<f32>",
+                "kernel": "conv_pipe<bf16> (all implicit-GEMM conv launches of a forward)" if args.precision == "bf16" else "conv_pipe<f32>",
                 "avg_launch_ms": round(avg_ms, 4), "launches_per_forward": cen["conv_launches"],
                 "conv_share_of_forward": round(cen["conv_ms"] / cen["total_ms"], 4),
                 "forward_ms": round(cen["total_ms"], 3),

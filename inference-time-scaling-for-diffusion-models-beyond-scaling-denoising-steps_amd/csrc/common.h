@@ -8,6 +8,7 @@ namespace itsd {
 
 extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_set_option)
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
+extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
 
@@ -85,6 +86,7 @@ struct ConvArgs {
   int* splitk_cnt;                   // per-tile arrival tickets (zero between launches)
   long long splitk_cap;
   int splitk_tiles;                  // ticket capacity
+  const float* gn_coef;              // fused GN+SiLU input transform coef[img][Cin/8][a0..7,b0..7] (bf16 3x3) or null
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -36,6 +36,7 @@ constexpr int TILEB = 128 * ROWB;
 constexpr int EROW = 132;  // epilogue LDS row (floats)
 constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + statistics partials
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
+int g_fuse_gn = 1;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_splitk = 1;        // split-K for under-filled grids (variant 2)
 
@@ -93,26 +94,30 @@ __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (
 template <typename T>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int tileP,
                                               int tileC) {
+  // waves 0..3 own the 128x128 accumulator tile; a block may have more threads (NT)
   constexpr int EPC = 16 / (int)sizeof(T);
+  const int NT = blockDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
+  const int wm = (wid >> 1) & 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
   const int HWo = a.Hout * a.Wout;
   float* E = (float*)smem;
+  if (tid < 256) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-        *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
-      }
+        for (int g = 0; g < 4; ++g) {
+          f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
+        }
+  }
   __syncthreads();
   if (a.vt_out && tileC >= a.vt_from) {
     // channel-major store of this (whole-V) tile: vt[img][c][pixel], 16-B chunks of
     // consecutive pixels of one image (host: HWo % EPC == 0, vt_from % 128 == 0); + bias only.
     const int Cv = a.Cout - a.vt_from;
-    for (int it = tid; it < 128 * (128 / EPC); it += 256) {
+    for (int it = tid; it < 128 * (128 / EPC); it += NT) {
       const int cl = it / (128 / EPC), pl = (it - cl * (128 / EPC)) * EPC;
       const int co = tileC + cl, p = tileP + pl;
       if (co >= a.Cout || p >= a.M) continue;
@@ -128,7 +133,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
   }
   const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
   constexpr int CPR = 128 / EPC;  // 16-B output chunks per tile row
-  for (int it = tid; it < 128 * CPR; it += 256) {
+  for (int it = tid; it < 128 * CPR; it += NT) {
     const int pl = it / CPR, cl = (it - pl * CPR) * EPC;
     const int p = tileP + pl, co = tileC + cl;
     if (p >= a.M || co >= a.Cout) continue;
@@ -190,7 +195,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     if (Gt >= 16) {
       // pass 1: 8 groups of 16 pixel rows x 32 channel quads, 16-B LDS reads
       float* R = E + 128 * EROW;  // [8 groups][2][128]
-      {
+      if (tid < 256) {
         const int cq = tid & 31, pg = tid >> 5;
         f32x4 s4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
         for (int k = 0; k < 16; ++k) {
@@ -207,7 +212,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
       __syncthreads();
       // pass 2: groups -> slots in fixed order (deterministic)
       const int gps = Gt / 16;
-      for (int item = tid; item < S * 128; item += 256) {
+      for (int item = tid; item < S * 128; item += NT) {
         const int s = item >> 7, cl = item & 127;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
@@ -221,7 +226,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
     } else {
-      for (int item = tid; item < S * 128; item += 256) {
+      for (int item = tid; item < S * 128; item += NT) {
         const int s = item >> 7, cl = item & 127;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
@@ -551,8 +556,254 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs a) {
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
+// ---------------------------------------------------------------------------- fused GN + SiLU + conv3x3
+// ResBlock block1/block2 (Model.py:170-174,179-184): conv3x3(silu(groupnorm(x))) with the
+// GroupNorm applied while the input tile is staged, so the normalised tensor never
+// exists in HBM. bf16, stride 1, pad 1, 64-channel K-chunks.
+//
+// Block = 8 waves, output tile 128 couts x 128 pixels (whole image rows; several
+// small images per tile). Waves 0-3 ("MFMA waves", 2x2 of 64x64) consume:
+//   * the weights as 9 taps x (Cin/64) stages of [128 couts][64 k] (16 KB) through a
+//     3-deep global_load_lds ring (counted vmcnt + raw barrier, as conv_pipe);
+//   * the input as a HALO image in LDS: the tile's rows plus a 1-pixel border,
+//     [halo pixel][64 ch] bf16 with the (row>>1)&7 chunk swizzle. The 9 taps are just
+//     9 shifted windows of it, so every input element is loaded from L2/HBM once per
+//     chunk instead of 9 times (implicit im2col).
+// Waves 4-7 ("loader waves") prepare the next chunk's halo in the other halo buffer:
+// 16-B loads to registers at tap 0, per-(image, channel) GN coefficients (a, b) to
+// LDS at tap 2, y = silu(x*a + b) -> bf16 -> LDS at tap 4 (padding stays exactly 0,
+// the conv pads the activated tensor). Their loads never enter the MFMA waves'
+// vmcnt accounting (vmcnt is per wave), and their VALU work co-issues beside the
+// MFMA waves' matrix work on the same SIMDs.
+constexpr int GNC_HALO_MAX = 288;                 // halo pixels per 128-pixel tile (4x4 images: 8 x 6x6)
+constexpr int GNC_HALO_BYTES = GNC_HALO_MAX * 128;
+constexpr int GNC_NS = 3;                          // weight ring depth
+constexpr int GNC_COEF_FLOATS = 8 * 64 * 2;        // [seg][64 ch][a|b] per chunk
+constexpr int GNC_SMEM = 2 * GNC_HALO_BYTES + GNC_NS * TILEB + 2 * GNC_COEF_FLOATS * 4;
+static_assert(GNC_SMEM >= EPI_BYTES, "epilogue reuses the fused conv's LDS");
+
+__global__ __launch_bounds__(512, 1) void conv3x3_gn_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  __shared__ __attribute__((aligned(16))) char smem[GNC_SMEM];
+  char* halo0 = smem;
+  char* wring = smem + 2 * GNC_HALO_BYTES;
+  float* coefl = (float*)(wring + GNC_NS * TILEB);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * CONV_BN, tileC = bt.y * CONV_BM;
+  const int H = a.Hout, W = a.Wout, HW = H * W, W2 = W + 2;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64, nS = 9 * ncc;
+  const int THs = min(H, 128 / W), segs = 128 / (THs * W), HS = (THs + 2) * W2, NH = segs * HS;
+  const int nimg = a.M / HW;
+  const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
+  const T* zero = (const T*)a.zero;
+
+  f32x16 acc[2][2];
+  zero_acc(acc);
+
+  if (wid < 4) {
+    // ================================================================ MFMA waves
+    const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
+    int hb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pl = wn * 64 + j * 32 + rl;
+      const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
+      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+    }
+    const T* arow[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * (4 * wid + q) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int co = tileC + r;
+      arow[q] = co < a.Cout ? (const T*)a.wt + (size_t)co * a.K + c * 8 : nullptr;
+    }
+    auto issue_w = [&](int s) {
+      const int cc = s / 9, tap = s - cc * 9;
+      const int k0 = tap * Cin + cc * 64;
+      char* dst = wring + (s % GNC_NS) * TILEB;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const T* ga = arow[q] ? arow[q] + k0 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(dst + (4 * wid + q) * 1024), 16, 0, 0);
+      }
+    };
+    issue_w(0);
+    if (nS > 1) issue_w(1);
+    __syncthreads();  // prologue barrier 1 (loaders stored chunk-0 coefficients)
+    for (int s = 0; s < nS; ++s) {
+      if (s + 1 < nS) wait_vmcnt<4>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < nS) issue_w(s + 2);
+      const int cc = s / 9, tap = s - cc * 9, ky = tap / 3, kx = tap - ky * 3;
+      const char* A = wring + (s % GNC_NS) * TILEB;
+      const char* Bh = halo0 + (cc & 1) * GNC_HALO_BYTES;
+      const int toff = ky * W2 + kx;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 af[2], bfg[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int h = hb[j] + toff;
+          bfg[j] = *(const bf16x8*)(Bh + h * 128 + ((((2 * kk + hh) ^ ((h >> 1) & 7))) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    wait_vmcnt<0>();
+  } else {
+    // ================================================================ loader waves
+    const int lt = tid - 256, lch = lt & 7;
+    int poff[9];  // pixel index (img*H + iy)*W + ix of item j, or -1 for padding / beyond NH
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int h = (lt >> 3) + 32 * j;
+      int po = -1;
+      if (h < NH) {
+        const int seg = h / HS, r = h - seg * HS, hy = r / W2, hx = r - hy * W2;
+        const int img = img0 + seg, iy = (segs > 1 ? 0 : y0) + hy - 1, ix = hx - 1;
+        if (img < nimg && iy >= 0 && iy < H && ix >= 0 && ix < W) po = (img * H + iy) * W + ix;
+      }
+      poff[j] = po;
+    }
+    const int cseg = lt >> 5, ck = (lt & 31) >> 2, cpart = lt & 3;  // coefficient f32x4 this thread moves
+    u32x4 hreg[9];
+    f32x4 creg;
+    auto load_chunk = [&](int cc) {
+      const int ci0 = cc * 64;
+      const bool s1 = ci0 < a.C1;
+      const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+      const int Cs = s1 ? a.C1 : a.C2;
+      const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const T* g = poff[j] >= 0 ? src + (size_t)poff[j] * Cs + cs0 : zero;
+        hreg[j] = *(const u32x4*)g;
+      }
+      const int img = img0 + cseg;
+      const float* cg = a.gn_coef + ((size_t)(img < nimg ? img : 0) * (Cin / 8) + cc * 8 + ck) * 16 + cpart * 4;
+      creg = (cseg < segs) ? *(const f32x4*)cg : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto store_coef = [&](int buf) {
+      *(f32x4*)(coefl + buf * GNC_COEF_FLOATS + lt * 4) = creg;  // == [seg][k][16] layout
+    };
+    auto write_halo = [&](int buf) {
+      const float* cf = coefl + buf * GNC_COEF_FLOATS;
+      char* hbuf = halo0 + buf * GNC_HALO_BYTES;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int h = (lt >> 3) + 32 * j;
+        if (h >= NH) continue;
+        u32x4 y = {0u, 0u, 0u, 0u};
+        if (poff[j] >= 0) {
+          const int seg = h / HS;
+          const float* c16 = cf + (seg * 8 + lch) * 16;  // a[8] then b[8]
+          const T* xe = (const T*)&hreg[j];
+          T* ye = (T*)&y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ye[e] = f2bf(silu(bf2f(xe[e]) * c16[e] + c16[8 + e]));
+        }
+        *(u32x4*)(hbuf + h * 128 + ((lch ^ ((h >> 1) & 7)) << 4)) = y;
+      }
+    };
+    // prologue: chunk 0 coefficients, barrier, chunk 0 halo
+    load_chunk(0);
+    store_coef(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // prologue barrier 1
+    write_halo(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int s = 0; s < nS; ++s) {
+      __builtin_amdgcn_s_barrier();
+      const int cc = s / 9, tap = s - cc * 9;
+      if (cc + 1 < ncc) {
+        if (tap == 0) load_chunk(cc + 1);
+        else if (tap == 2) {
+          store_coef((cc + 1) & 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (tap == 4) {
+          write_halo((cc + 1) & 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      }
+    }
+  }
+  __syncthreads();
+  conv_epilogue<T>(a, acc, smem, tileP, tileC);
+}
+
+// GroupNorm finalize for the fused conv: per (image, channel) a = rstd*gamma,
+// b = beta - mean*a from the producers' statistics slabs (same fp64 group reduction
+// as gn_apply_kernel), written as coef[img][C/8][a0..a7, b0..b7].
+__global__ __launch_bounds__(256) void gn_finalize_kernel(GNArgs a, float* coef) {
+  __shared__ float gst[32][2];
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const int C = a.C1 + a.C2, gs = C / 32;
+  const int Gt = stat_slot_px(a.HW), spi = a.HW / Gt;
+  {
+    const int g = tid >> 3, l8 = tid & 7;
+    double s = 0.0, q = 0.0;
+    for (int k = l8; k < gs * spi; k += 8) {
+      const int c = g * gs + k / spi;
+      const long long sl = (long long)img * spi + (k % spi);
+      const float* st;
+      int Cs, cc;
+      if (c < a.C1) { st = a.st1; Cs = a.C1; cc = c; } else { st = a.st2; Cs = a.C2; cc = c - a.C1; }
+      s += (double)st[(sl * 2) * Cs + cc];
+      q += (double)st[(sl * 2 + 1) * Cs + cc];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+    if (l8 == 0) {
+      const double E = (double)gs * a.HW;
+      const double mean = s / E;
+      double var = q / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      gst[g][0] = (float)mean;
+      gst[g][1] = (float)(1.0 / sqrt(var + (double)a.eps));
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int g = c / gs;
+    const float sc = gst[g][1] * a.gamma[c];
+    float* o = coef + ((size_t)img * (C / 8) + c / 8) * 16 + (c & 7);
+    o[0] = sc;
+    o[8] = a.beta[c] - gst[g][0] * sc;
+  }
+}
+
+hipError_t launch_gn_finalize(const GNArgs& a, int n, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(n), dim3(256), 0, s, a, coef);
+  return hipGetLastError();
+}
+
+// Host-side eligibility of the fused kernel (the builder decides per ResBlock conv).
+bool conv_gn_eligible(int H, int W, int Cin) {
+  if (Cin % 64 || W > 128 || 128 % W) return false;
+  const int THs = std::min(H, 128 / W);
+  if ((THs * W) == 0 || 128 % (THs * W) || H % THs) return false;
+  const int segs = 128 / (THs * W);
+  return segs * (THs + 2) * (W + 2) <= GNC_HALO_MAX;
+}
+
 template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (a.gn_coef) {
+      dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+      hipLaunchKernelGGL(conv3x3_gn_kernel, grid, dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   constexpr int BK = 8 * (16 / (int)sizeof(T));
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
   const int Cin = a.C1 + a.C2;

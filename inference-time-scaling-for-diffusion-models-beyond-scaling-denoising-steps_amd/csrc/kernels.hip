@@ -55,16 +55,16 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
     coef[1][c] = a.beta[c] - gst[g][0] * sc;
   }
   __syncthreads();
-  const int cpp = C / EPC;  // chunks per pixel
-  const long long total = (long long)a.HW * cpp;
-  const long long c0 = (long long)blockIdx.x * a.chunks_per_block;
-  const long long c1 = min(total, c0 + a.chunks_per_block);
+  const unsigned cpp = C / EPC;  // chunks per pixel
+  const unsigned total = (unsigned)a.HW * cpp;
+  const unsigned c0 = blockIdx.x * (unsigned)a.chunks_per_block;
+  const unsigned c1 = min(total, c0 + (unsigned)a.chunks_per_block);
   const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
   const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
   T* dst = (T*)a.dst + (size_t)img * a.HW * C;
-  for (long long idx = c0 + tid; idx < c1; idx += 256) {
+  for (unsigned idx = c0 + tid; idx < c1; idx += 256) {
     const int p = (int)(idx / cpp);
-    const int c = (int)(idx - (long long)p * cpp) * EPC;
+    const int c = (int)(idx - (unsigned)p * cpp) * EPC;
     const u32x4 x = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c)
                              : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
     const T* xe = (const T*)&x;
@@ -299,19 +299,21 @@ template hipError_t launch_attn<bf16_t>(const AttnArgs&, int, hipStream_t);
 template <typename T>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);
-  extern __shared__ float hw[];  // [Cout][27] then bias [Cout]
-  for (int i = threadIdx.x; i < a.Cout * 27; i += 256) hw[i] = a.w[i];
+  extern __shared__ __attribute__((aligned(16))) float hw[];  // [27][Cout] (k-major: 16-B reads) then bias [Cout]
+  for (int i = threadIdx.x; i < a.Cout * 27; i += 256) {
+    const int co = i / 27, k = i - co * 27;
+    hw[k * a.Cout + co] = a.w[i];
+  }
   for (int i = threadIdx.x; i < a.Cout; i += 256) hw[a.Cout * 27 + i] = a.b[i];
   __syncthreads();
   const int HW = a.H * a.W;
-  const int cq = a.Cout / EPC;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)a.n * HW * cq;
-  if (idx >= total) return;
-  const int c0 = (int)(idx % cq) * EPC;
-  const long long pix = idx / cq;
-  const int img = (int)(pix / HW);
-  const int rem = (int)(pix - (long long)img * HW);
+  const unsigned cq = a.Cout / EPC;
+  const unsigned idx = blockIdx.x * 256u + threadIdx.x;  // host: n*HW*cq < 2^31
+  if (idx >= (unsigned)a.n * HW * cq) return;
+  const unsigned pix = idx / cq;
+  const int c0 = (int)(idx - pix * cq) * EPC;
+  const int img = (int)(pix / (unsigned)HW);
+  const int rem = (int)(pix - (unsigned)img * HW);
   const int y = rem / a.W, x = rem - y * a.W;
   const float* xs = a.x + (size_t)(img % a.x_img_mod) * 3 * HW;
   float in[27];
@@ -324,16 +326,22 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
         const int iy = y + ky - 1, ix = x + kx - 1;
         in[ci * 9 + ky * 3 + kx] = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? xs[ci * HW + iy * a.W + ix] : 0.0f;
       }
+  float acc[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) acc[e] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+#pragma unroll
+    for (int q = 0; q < EPC / 4; ++q) {
+      const f32x4 w4 = *(const f32x4*)(hw + k * a.Cout + c0 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * q + e] = fmaf(w4[e], in[k], acc[4 * q + e]);
+    }
+  }
   u32x4 w;
   T* we = (T*)&w;
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) {
-    const float* wr = hw + (c0 + e) * 27;
-    float acc = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 27; ++k) acc = fmaf(wr[k], in[k], acc);
-    we[e] = Elem<T>::to(acc + hw[a.Cout * 27 + c0 + e]);
-  }
+  for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(acc[e] + hw[a.Cout * 27 + c0 + e]);
   *(u32x4*)((T*)a.out + (size_t)pix * a.Cout + c0) = w;
 }
 
@@ -478,10 +486,12 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
   }
   const int bpi = H / rpb;
   const int img = blockIdx.x / bpi, y0 = (blockIdx.x % bpi) * rpb;
-  const int tid = threadIdx.x, pl = tid >> 2, cq = tid & 3;
+  // wave = channel quarter (its weight reads are wave-uniform LDS broadcasts),
+  // lane = output pixel (halo reads at a conflict-free padded pixel stride)
+  const int tid = threadIdx.x, pl = tid & 63, cq = tid >> 6;
   const int py = pl / W, px = pl - (pl / W) * W;
   const int cpq = C / 4;
-  float eps[3] = {0.f, 0.f, 0.f}, unc[3] = {0.f, 0.f, 0.f};
+  float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);  // [2 passes][4 waves][64 px][3]
   for (int pass = 0; pass < (a.cfg ? 2 : 1); ++pass) {
     const int im = img + pass * a.n;
     __syncthreads();
@@ -505,32 +515,40 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
           const u32x4 v = *(const u32x4*)(hpix + c * (int)sizeof(T));
           const T* ve = (const T*)&v;
 #pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            const float gv = Elem<T>::tof(ve[e]);
-            s0 = fmaf(gv, wp[(c + e) * 3 + 0], s0);
-            s1 = fmaf(gv, wp[(c + e) * 3 + 1], s1);
-            s2 = fmaf(gv, wp[(c + e) * 3 + 2], s2);
+          for (int e0 = 0; e0 < EPC; e0 += 4) {
+            const f32x4 w0 = *(const f32x4*)(wp + (c + e0) * 3);      // 12 consecutive weights:
+            const f32x4 w1 = *(const f32x4*)(wp + (c + e0) * 3 + 4);  // 4 channels x 3 outputs
+            const f32x4 w2 = *(const f32x4*)(wp + (c + e0) * 3 + 8);
+            const float g0 = Elem<T>::tof(ve[e0]), g1 = Elem<T>::tof(ve[e0 + 1]);
+            const float g2 = Elem<T>::tof(ve[e0 + 2]), g3 = Elem<T>::tof(ve[e0 + 3]);
+            s0 = fmaf(g0, w0[0], s0); s1 = fmaf(g0, w0[1], s1); s2 = fmaf(g0, w0[2], s2);
+            s0 = fmaf(g1, w0[3], s0); s1 = fmaf(g1, w1[0], s1); s2 = fmaf(g1, w1[1], s2);
+            s0 = fmaf(g2, w1[2], s0); s1 = fmaf(g2, w1[3], s1); s2 = fmaf(g2, w2[0], s2);
+            s0 = fmaf(g3, w2[1], s0); s1 = fmaf(g3, w2[2], s1); s2 = fmaf(g3, w2[3], s2);
           }
         }
       }
-#pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {
-      s0 += __shfl_xor(s0, o, 64);
-      s1 += __shfl_xor(s1, o, 64);
-      s2 += __shfl_xor(s2, o, 64);
-    }
-    float* dst = pass ? unc : eps;
-    dst[0] = s0 + a.b[0]; dst[1] = s1 + a.b[1]; dst[2] = s2 + a.b[2];
+    float* rp = red + ((pass * 4 + cq) * 64 + pl) * 3;
+    rp[0] = s0; rp[1] = s1; rp[2] = s2;
   }
-  if (cq >= 3) return;
-  float e = cq == 0 ? eps[0] : (cq == 1 ? eps[1] : eps[2]);
+  __syncthreads();
+  if (tid >= 192) return;
+  const int opx = tid / 3, oc = tid - opx * 3;  // (pixel, output channel), channel quarters summed in order
+  float e = a.b[oc];
+  {
+    float s = 0.f;
+    for (int w = 0; w < 4; ++w) s += red[(w * 64 + opx) * 3 + oc];
+    e += s;
+  }
   if (a.cfg) {
 #pragma clang fp contract(off)
-    const float u = cq == 0 ? unc[0] : (cq == 1 ? unc[1] : unc[2]);
+    float s = 0.f;
+    for (int w = 0; w < 4; ++w) s += red[((4 + w) * 64 + opx) * 3 + oc];
+    const float u = a.b[oc] + s;
     e = a.guide_w1 * e - a.guide_w * u;
   }
-  const int rem = (y0 + py) * W + px;
-  const size_t o = ((size_t)img * 3 + cq) * HW + rem;
+  const int rem = (y0 + opx / W) * W + (opx - (opx / W) * W);
+  const size_t o = ((size_t)img * 3 + oc) * HW + rem;
   if (!a.step_mode) {
     a.eps_out[o] = e;
     return;
@@ -555,7 +573,7 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 template <typename T>
 hipError_t launch_tail(const TailArgs& a, hipStream_t s) {
   if (a.W <= 64 && 64 % a.W == 0 && a.H % (64 / a.W) == 0 && a.C % 32 == 0) {
-    const size_t sm = 27 * a.C * 4 + (size_t)(64 / a.W + 2) * (a.W + 2) * (a.C * sizeof(T) + 16);
+    const size_t sm = 27 * a.C * 4 + (size_t)(64 / a.W + 2) * (a.W + 2) * (a.C * sizeof(T) + 16) + 2 * 4 * 64 * 3 * 4;
     if (sm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {

@@ -24,7 +24,10 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
+    ap.add_argument("--fuse-gn", type=int, default=1, help="fused GroupNorm+SiLU+conv3x3 in ResBlocks")
     args = ap.parse_args()
+    from itsd import runtime as rt
+    rt.set_option("fuse_gn", args.fuse_gn)
     a = ARCH_A
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=args.precision, weights="gauss")
     net.to("cuda:0")
