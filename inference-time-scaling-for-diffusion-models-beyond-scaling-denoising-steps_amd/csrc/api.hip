@@ -34,8 +34,7 @@ hipError_t launch_linear(const float*, int, int, const float*, const float*, int
 hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hipStream_t);
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
-hipError_t launch_gn_finalize(const GNArgs&, int, float*, hipStream_t);
-bool conv_gn_eligible(int H, int W, int Cin);
+bool conv_gn_eligible(int H, int W);
 hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
                         hipStream_t);
 }  // namespace itsd
@@ -78,7 +77,7 @@ struct Act {
   size_t stats = SIZE_MAX;  // ws offset of the channel-statistics slab (consumed by a GroupNorm), or none
 };
 
-enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNFIN };
+enum OpKind { OP_GN, OP_CONV, OP_ATTN };
 
 struct Op {
   OpKind kind;
@@ -95,7 +94,7 @@ struct Op {
   // ATTN
   int S = 0, C = 0;
   int vt = -1, vt_from = 0;  // channel-major V buffer (conv: couts >= vt_from go there; attn: reads it)
-  size_t coef = SIZE_MAX;    // GNFIN: output coef buffer; CONV: fused GN+SiLU input coefficients
+  int gnfuse = 0;            // CONV: GroupNorm(gamma, beta)+SiLU of the input fused into the conv
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -269,28 +268,29 @@ struct Builder {
     u->ops.push_back(o);
   }
   int conv_layer(int s1, int s2, const std::string& name, int Cout, int ks, int stride, int pad, int ups, int Hout,
-                 int Wout, int temb_col = -1, int resid = -1, size_t gn_coef = SIZE_MAX) {
+                 int Wout, int temb_col = -1, int resid = -1, const std::string& gn = "") {
     const int Cin = u->acts[s1].C + (s2 >= 0 ? u->acts[s2].C : 0);
+    size_t gg = 0, gb = 0;
+    if (!gn.empty()) {
+      gg = f32(gn + ".weight", Cin);
+      gb = f32(gn + ".bias", Cin);
+    }
     const float* W = get(name + ".weight", (int64_t)Cout * Cin * ks * ks);
     size_t wt = pack({W}, Cout, Cin, ks);
     size_t b = f32(name + ".bias", Cout);
     int dst = act(Hout, Wout, Cout);
     conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
-    u->ops.back().coef = gn_coef;
+    if (!gn.empty()) {
+      Op& o = u->ops.back();
+      o.gnfuse = 1; o.gamma = gg; o.beta = gb;
+    }
     return dst;
   }
-  // GroupNorm finalize op: per-(image, channel) scale/shift for a fused conv; returns
-  // the ws offset of its coef buffer [nb_max][C/8][16] fp32.
-  size_t gnfin(int s1, int s2, const std::string& p, int C) {
-    Op o;
-    o.kind = OP_GNFIN;
-    o.src1 = s1; o.src2 = s2;
-    o.gamma = f32(p + ".weight", C);
-    o.beta = f32(p + ".bias", C);
-    o.coef = ws_off;
-    ws_off = (ws_off + (size_t)u->nb_max * C * 2 * 4 + 255) & ~(size_t)255;
-    u->ops.push_back(o);
-    return o.coef;
+  // conv3x3(silu(GroupNorm(s1 ++ s2))) can run as one fused launch (conv3x3_gn_kernel)
+  bool fusable(int s1, int s2, int Cout) const {
+    const Act& A = u->acts[s1];
+    return u->bf16 && itsd::g_fuse_gn && A.C % 64 == 0 && (s2 < 0 || u->acts[s2].C % 64 == 0) &&
+           Cout % 128 == 0 && conv_gn_eligible(A.H, A.W);
   }
 
   int resblock(int x1, int x2, const std::string& p, int in_ch, int out_ch, bool attn) {
@@ -298,25 +298,26 @@ struct Builder {
     const int col = u->sumC;
     u->sumC += out_ch;
     temb_cols.push_back({p, (size_t)col});
-    const bool fuse = u->bf16 && itsd::g_fuse_gn && conv_gn_eligible(H, W, in_ch) && conv_gn_eligible(H, W, out_ch);
+    // GroupNorm+SiLU either fused into the conv's input staging (conv3x3_gn_kernel) or
+    // materialised by gn_apply_kernel
     int h1, o;
     int resid = x1;
-    if (fuse) {
-      // GroupNorm+SiLU applied inside the conv's input staging (conv3x3_gn_kernel)
-      size_t c1 = gnfin(x1, x2, p + ".block1.0", in_ch);
-      h1 = conv_layer(x1, x2, p + ".block1.2", out_ch, 3, 1, 1, 0, H, W, col, -1, c1);
-      size_t c2 = gnfin(h1, -1, p + ".block2.0", out_ch);
-      if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
-      o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, c2);
+    if (fusable(x1, x2, out_ch)) {
+      h1 = conv_layer(x1, x2, p + ".block1.2", out_ch, 3, 1, 1, 0, H, W, col, -1, p + ".block1.0");
     } else {
       int g1 = act(H, W, in_ch);
       gn(x1, x2, g1, p + ".block1.0", in_ch, 1);
       h1 = conv_layer(g1, -1, p + ".block1.2", out_ch, 3, 1, 1, 0, H, W, col);
-      int g2 = act(H, W, out_ch);
-      gn(h1, -1, g2, p + ".block2.0", out_ch, 1);
-      if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
-      o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
     }
+    const bool f2 = fusable(h1, -1, out_ch);
+    int g2 = -1;
+    if (!f2) {
+      g2 = act(H, W, out_ch);
+      gn(h1, -1, g2, p + ".block2.0", out_ch, 1);
+    }
+    if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
+    if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
+    else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
     if (attn) {
       const std::string a = p + ".attn";
       int ga = act(H, W, out_ch);
@@ -479,7 +480,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   {
     std::vector<int> need;
     for (const Op& o : u->ops)
-      if (o.kind == OP_GN || o.kind == OP_GNFIN) {
+      if (o.kind == OP_GN || (o.kind == OP_CONV && o.gnfuse)) {
         need.push_back(o.src1);
         if (o.src2 >= 0) need.push_back(o.src2);
       }
@@ -527,21 +528,7 @@ struct RunCtx {
 
 int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
   hipError_t e = hipSuccess;
-  if (o.kind == OP_GNFIN) {
-    GNArgs a{};
-    a.src1 = u->ap(o.src1);
-    a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
-    a.C1 = u->acts[o.src1].C;
-    a.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
-    a.HW = u->acts[o.src1].H * u->acts[o.src1].W;
-    a.gamma = u->wp(o.gamma);
-    a.beta = u->wp(o.beta);
-    a.eps = 1e-5f;
-    a.silu = 1;
-    a.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
-    a.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
-    e = launch_gn_finalize(a, c.nb, (float*)(u->ws + o.coef), s);
-  } else if (o.kind == OP_GN) {
+  if (o.kind == OP_GN) {
     GNArgs a{};
     a.src1 = u->ap(o.src1);
     a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
@@ -597,11 +584,14 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
       a.vt_from = o.vt_from;
     }
     a.zins = o.zins;
-    if (o.coef != SIZE_MAX) {
-      if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.upsample || o.zins || !conv_gn_eligible(in.H, in.W, a.C1 + a.C2) ||
-          a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
+    if (o.gnfuse) {
+      if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
+          !conv_gn_eligible(in.H, in.W) || a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
         return fail(ITSD_ERR_INVALID, "internal: fused GroupNorm conv on an unsupported shape");
-      a.gn_coef = (const float*)(u->ws + o.coef);
+      a.gn_gamma = u->wp(o.gamma);
+      a.gn_beta = u->wp(o.beta);
+      a.gn_st1 = (const float*)(u->ws + in.stats);
+      a.gn_st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
     }
     {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
       const int epc = u->bf16 ? 8 : 4;
@@ -1018,7 +1008,7 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
       for (int q = 0; q < 6; ++q) sh[q] = 0;
       if (i >= 1 && i - 1 < u->ops.size()) {
         const Op& o = u->ops[i - 1];
-        const Act& out = u->acts[o.dst >= 0 ? o.dst : o.src1];
+        const Act& out = u->acts[o.dst];
         const Act& in = u->acts[o.src1];
         sh[0] = n * out.H * out.W;
         sh[1] = o.kind == OP_CONV ? o.Cout : out.C;

@@ -86,7 +86,12 @@ struct ConvArgs {
   int* splitk_cnt;                   // per-tile arrival tickets (zero between launches)
   long long splitk_cap;
   int splitk_tiles;                  // ticket capacity
-  const float* gn_coef;              // fused GN+SiLU input transform coef[img][Cin/8][a0..7,b0..7] (bf16 3x3) or null
+  // fused GroupNorm+SiLU of the input (bf16 3x3, conv3x3_gn_kernel): gamma/beta [Cin] and the
+  // sources' statistics slabs; null gamma = plain conv
+  const float* gn_gamma;
+  const float* gn_beta;
+  const float* gn_st1;
+  const float* gn_st2;
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of
