@@ -25,7 +25,6 @@
 namespace itsd {
 template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
 template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
-template <typename T> hipError_t launch_stats(const void*, int, int, int, float*, hipStream_t);
 template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
@@ -153,11 +152,9 @@ struct itsd_unet {
   float guide_w = 0.f, guide_w1 = 1.f;
   int* d_t = nullptr;
   int* d_nan = nullptr;
-  void* zero_page = nullptr;  // 1 KiB of zeros (conv DMA source for padding)
+  void* zero_page = nullptr;  // 256 KiB of zeros (conv DMA source for padding, conv.hip zero_of_block)
   float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
-  int* splitk_cnt = nullptr;   // per-tile tickets, zeroed once; each launch's last arriver resets its own
   static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
-  static constexpr int kSplitkTiles = 65536;
 
   hipStream_t stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
@@ -575,9 +572,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.zero = u->zero_page;
     a.splitk_ws = u->splitk_ws;
-    a.splitk_cnt = u->splitk_cnt;
     a.splitk_cap = itsd_unet::kSplitkCap;
-    a.splitk_tiles = itsd_unet::kSplitkTiles;
     if (o.vt >= 0) {
       if (o.vt_from % 128 || (out.H * out.W) % 8) return fail(ITSD_ERR_INVALID, "internal: bad channel-major V split");
       a.vt_out = u->ap(o.vt);
@@ -643,13 +638,9 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     h.b = u->wp(u->head_b);
     h.out = u->ap(u->head_out);
     h.H = u->H; h.W = u->H; h.Cout = u->ch; h.n = c.nb; h.x_img_mod = c.x_mod;
-    hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
     const Act& ho = u->acts[u->head_out];
-    if (e == hipSuccess && ho.stats != SIZE_MAX) {
-      float* st = (float*)(u->ws + ho.stats);
-      e = u->bf16 ? launch_stats<bf16_t>(h.out, c.nb * u->H * u->H, u->ch, u->H * u->H, st, s)
-                  : launch_stats<float>(h.out, c.nb * u->H * u->H, u->ch, u->H * u->H, st, s);
-    }
+    h.stats = ho.stats != SIZE_MAX ? (float*)(u->ws + ho.stats) : nullptr;
+    hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   for (const Op& o : u->ops) CHK(mark((int)o.kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
@@ -732,7 +723,8 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "splitk")) {
-    itsd::g_splitk = value ? 1 : 0;
+    if (value < 0 || value > 64) return fail(ITSD_ERR_INVALID, "splitk in [0,64]");
+    itsd::g_splitk = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
@@ -770,11 +762,9 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipEventCreateWithFlags(&u->ev_out, hipEventDisableTiming));
   HIPCHK(hipMalloc(&u->d_t, 64));
   HIPCHK(hipMalloc(&u->d_nan, 64));
-  HIPCHK(hipMalloc(&u->zero_page, 1024));
-  HIPCHK(hipMemset(u->zero_page, 0, 1024));
+  HIPCHK(hipMalloc(&u->zero_page, 64 * 4096 + 1024));
+  HIPCHK(hipMemset(u->zero_page, 0, 64 * 4096 + 1024));
   HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
-  HIPCHK(hipMalloc(&u->splitk_cnt, itsd_unet::kSplitkTiles * 4));
-  HIPCHK(hipMemset(u->splitk_cnt, 0, itsd_unet::kSplitkTiles * 4));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -793,7 +783,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   hipFree(u->wdev); hipFree(u->ws); hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
   hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
   hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->zero_page);
-  hipFree(u->splitk_ws); hipFree(u->splitk_cnt);
+  hipFree(u->splitk_ws);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
   if (u->ev_out) hipEventDestroy(u->ev_out);

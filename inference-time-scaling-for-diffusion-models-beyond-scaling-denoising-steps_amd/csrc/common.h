@@ -83,9 +83,7 @@ struct ConvArgs {
   void* vt_out;                      // couts >= vt_from go channel-major to vt_out[img][co-vt_from][HWo]
   int vt_from;                       // (the V of a fused q|k|v projection, for the MFMA attention)
   float* splitk_ws;                  // split-K partial tiles (capacity splitk_cap floats) or null
-  int* splitk_cnt;                   // per-tile arrival tickets (zero between launches)
   long long splitk_cap;
-  int splitk_tiles;                  // ticket capacity
   // fused GroupNorm+SiLU of the input (bf16 3x3, conv3x3_gn_kernel): gamma/beta [Cin] and the
   // sources' statistics slabs; null gamma = plain conv
   const float* gn_gamma;
@@ -124,6 +122,7 @@ struct HeadArgs {
   void* out;            // NHWC [n][H][W][Cout]
   int H, W, Cout, n;
   int x_img_mod;        // image i reads x[i % x_img_mod] (CFG cond||uncond batch)
+  float* stats;         // GroupNorm statistics slab of the output [slot][2][Cout], or null
 };
 
 struct TailArgs {

@@ -38,7 +38,7 @@ constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + stat
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
 int g_fuse_gn = 1;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
-int g_splitk = 1;        // split-K for under-filled grids (variant 2)
+int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -283,12 +283,23 @@ __device__ __forceinline__ TileId tile_of_block() {
   return id;
 }
 
-__device__ __forceinline__ bool splitk_reduce(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int z, int S,
-                                              const TileId& bt) {
-  const int tid = threadIdx.x;
-  const long long tile = (long long)bt.y * gridDim.x + bt.x;
-  float* slab = a.splitk_ws + (size_t)tile * S * 16384;
-  float* mine = slab + (size_t)z * 16384 + tid * 64;
+// Padding rows are DMA'd from a zero region. One shared 16-B source would put every
+// padded row of every CU on the same L2 channel (at the 4x4 level ~1/3 of all taps are
+// padding); each block reads its own 4-KiB-spaced slot of a 256-KiB region instead.
+template <typename T>
+__device__ __forceinline__ const T* zero_of_block(const ConvArgs& a) {
+  const int b = blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z;
+  return (const T*)((const char*)a.zero + (b & 63) * 4096);
+}
+
+// Split-K (under-filled grids): slice z of a tile writes its raw fp32 accumulators to
+// slab[tile][z][thread][64] and exits; splitk_epilogue_kernel (next launch on the stream,
+// so no cross-XCD fences) sums the slices in slice order -- deterministic -- and runs
+// the shared epilogue. Slab index of a tile: y * gridDim.x + x.
+__device__ __forceinline__ void splitk_store(const ConvArgs& a, f32x16 (&acc)[2][2], int z, int S, const TileId& bt,
+                                             int gx) {
+  const long long tile = (long long)bt.y * gx + bt.x;
+  float* mine = a.splitk_ws + ((size_t)tile * S + z) * 16384 + threadIdx.x * 64;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -298,45 +309,6 @@ __device__ __forceinline__ bool splitk_reduce(const ConvArgs& a, f32x16 (&acc)[2
         f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
         *(f32x4*)(mine + (i * 2 + j) * 16 + 4 * g) = v;
       }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = (int*)smem;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(a.splitk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == S - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      a.splitk_cnt[tile] = 0;
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  const int last = *flag;
-  __syncthreads();
-  if (!last) return false;
-  f32x16 tot[2][2];
-  zero_acc(tot);
-  for (int zz = 0; zz < S; ++zz) {
-    const float* src = slab + (size_t)zz * 16384 + tid * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = *(const f32x4*)(src + (i * 2 + j) * 16 + 4 * g);  // own slice too (same values)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) tot[i][j][4 * g + e] += v[e];
-        }
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
-  return true;
 }
 
 // ---------------------------------------------------------------------------- pipelined
@@ -370,7 +342,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   const int HWo = a.Hout * a.Wout;
   const int Hv = a.upsample ? 2 * a.Hin : (a.zins ? 2 * a.Hin - 1 : a.Hin);
   const int Wv = a.upsample ? 2 * a.Win : (a.zins ? 2 * a.Win - 1 : a.Win);
-  const T* zero = (const T*)a.zero;
+  const T* zero = zero_of_block<T>(a);
 
   // This lane's DMA rows: instruction q of wave w fills rows 8*(4w+q) .. +7 (1 KiB);
   // lane L lands at row 8*(4w+q) + L/8, slot L%8, so it must fetch logical chunk
@@ -467,7 +439,32 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   }
   wait_vmcnt<0>();
   __syncthreads();
-  if (S > 1 && !splitk_reduce(a, acc, smem, z, S, bt)) return;
+  if (S > 1) {
+    splitk_store(a, acc, z, S, bt, gridDim.x);
+    return;
+  }
+  conv_epilogue<T>(a, acc, smem, tileP, tileC);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs a, int S) {
+  __shared__ __attribute__((aligned(16))) char smem[EPI_BYTES];
+  const int tileP = blockIdx.x * CONV_BN, tileC = blockIdx.y * CONV_BM;
+  const float* src = a.splitk_ws + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * S * 16384 + threadIdx.x * 64;
+  f32x16 acc[2][2];
+  zero_acc(acc);
+  for (int z = 0; z < S; ++z, src += 16384) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *(const f32x4*)(src + (i * 2 + j) * 16 + 4 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
+        }
+  }
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
@@ -610,7 +607,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   const int THs = min(H, 128 / W), segs = 128 / (THs * W), HS = (THs + 2) * W2, NH = segs * HS;
   const int nimg = a.M / HW;
   const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
-  const T* zero = (const T*)a.zero;
+  const T* zero = zero_of_block<T>(a);
 
   // ---- group statistics of the tile's images (fp64 over the slabs, fixed order)
   {
@@ -832,9 +829,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     const int blocks = (int)(grid.x * grid.y);
     const int nK = a.ksize * a.ksize * (Cin / BK);
     int S = 1;
-    if (blocks < 256) S = std::min((512 + blocks - 1) / blocks, nK / 8);  // measured: helps only < 1 block/CU
+    if (g_splitk >= 2) S = std::min(g_splitk, nK / 4);  // forced slice count (measurements)
+    else if (blocks < 256) S = std::min((512 + blocks - 1) / blocks, nK / 8);  // measured: helps only < 1 block/CU
     while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
-    if (blocks > a.splitk_tiles) S = 1;
     grid.z = S < 1 ? 1 : S;
   }
   if (!pipe || v == 1) hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
@@ -842,6 +839,11 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   else if (v == 2) hipLaunchKernelGGL((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
   else if (v == 3) hipLaunchKernelGGL((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
+  if (grid.z > 1) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(splitk_epilogue_kernel<T>, dim3(grid.x, grid.y), dim3(256), 0, s, a, (int)grid.z);
+  }
   return hipGetLastError();
 }
 

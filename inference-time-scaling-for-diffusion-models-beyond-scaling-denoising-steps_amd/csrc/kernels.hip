@@ -12,7 +12,7 @@ namespace itsd {
 // nn.GroupNorm(32, C, eps=1e-5) (Model.py:132,171,180,253) with optional Swish over
 // the channel concat of two NHWC sources (the up path's torch.cat, Model.py:280; a
 // group may straddle the two sources). The statistics come from the producers'
-// channel slabs (conv epilogue / stats_kernel): per image, the group's sum and sum
+// channel slabs (conv epilogue / head kernel): per image, the group's sum and sum
 // of squares are reduced in fp64 (fixed order: deterministic), mean/biased var ->
 // a = rstd*gamma, b = beta - mean*a per channel in LDS; the block then streams its
 // pixel range with 16-B loads/stores: y = silu(x*a + b).
@@ -93,33 +93,6 @@ hipError_t launch_groupnorm(const GNArgs& a0, int n, hipStream_t s) {
 template hipError_t launch_groupnorm<float>(const GNArgs&, int, hipStream_t);
 template hipError_t launch_groupnorm<bf16_t>(const GNArgs&, int, hipStream_t);
 
-// Channel-statistics slab of an NHWC tensor that no conv epilogue produced (the head
-// output): one block per slot of Gt pixels, one thread per channel.
-template <typename T>
-__global__ __launch_bounds__(256) void stats_kernel(const T* x, int M, int C, int HW, float* stats) {
-  const int Gt = stat_slot_px(HW);
-  const long long slot = blockIdx.x;
-  const long long p0 = slot * Gt;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f, q = 0.f;
-    for (int k = 0; k < Gt && p0 + k < M; ++k) {
-      const float v = Elem<T>::tof(x[(size_t)(p0 + k) * C + c]);
-      s += v;
-      q = fmaf(v, v, q);
-    }
-    stats[(slot * 2) * C + c] = s;
-    stats[(slot * 2 + 1) * C + c] = q;
-  }
-}
-
-template <typename T>
-hipError_t launch_stats(const void* x, int M, int C, int HW, float* stats, hipStream_t s) {
-  const int Gt = stat_slot_px(HW);
-  hipLaunchKernelGGL(stats_kernel<T>, dim3((M + Gt - 1) / Gt), dim3(256), 0, s, (const T*)x, M, C, HW, stats);
-  return hipGetLastError();
-}
-template hipError_t launch_stats<float>(const void*, int, int, int, float*, hipStream_t);
-template hipError_t launch_stats<bf16_t>(const void*, int, int, int, float*, hipStream_t);
 
 // ============================================================================ attention core
 // AttnBlock core (Model.py:152-161): w = softmax(q k^T * C^-0.5) ; h = w v, single head,
@@ -294,63 +267,109 @@ template hipError_t launch_attn<bf16_t>(const AttnArgs&, int, hipStream_t);
 
 // ============================================================================ head conv
 // head = Conv2d(3, ch, 3, padding=1) (Model.py:219) from the NCHW fp32 sampler state
-// to NHWC activations. One thread per (pixel, 16-B chunk of output channels);
-// consecutive threads cover one pixel's channel row (coalesced stores), weights in LDS.
+// to NHWC activations. A block covers one GroupNorm statistics slot (128 pixels);
+// threads are (pixel lane, 16-B chunk of output channels), consecutive threads one
+// pixel's channel row (coalesced stores), weights in LDS. The block also writes the
+// slot's channel sums / sums of squares for the first ResBlock's GroupNorm.
 template <typename T>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) float hw[];  // [27][Cout] (k-major: 16-B reads) then bias [Cout]
-  for (int i = threadIdx.x; i < a.Cout * 27; i += 256) {
-    const int co = i / 27, k = i - co * 27;
-    hw[k * a.Cout + co] = a.w[i];
+  float* red = hw + 28 * a.Cout;                              // [256 / cq][Cout][2] statistics partials
+  // fill in destination order: conflict-free LDS stores, gathered (L2-resident) reads
+  for (int d = threadIdx.x; d < a.Cout * 27; d += 256) {
+    const int k = d / a.Cout, co = d - k * a.Cout;
+    hw[d] = a.w[co * 27 + k];
   }
   for (int i = threadIdx.x; i < a.Cout; i += 256) hw[a.Cout * 27 + i] = a.b[i];
   __syncthreads();
-  const int HW = a.H * a.W;
-  const unsigned cq = a.Cout / EPC;
-  const unsigned idx = blockIdx.x * 256u + threadIdx.x;  // host: n*HW*cq < 2^31
-  if (idx >= (unsigned)a.n * HW * cq) return;
-  const unsigned pix = idx / cq;
-  const int c0 = (int)(idx - pix * cq) * EPC;
-  const int img = (int)(pix / (unsigned)HW);
-  const int rem = (int)(pix - (unsigned)img * HW);
-  const int y = rem / a.W, x = rem - y * a.W;
-  const float* xs = a.x + (size_t)(img % a.x_img_mod) * 3 * HW;
-  float in[27];
-#pragma unroll
-  for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iy = y + ky - 1, ix = x + kx - 1;
-        in[ci * 9 + ky * 3 + kx] = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? xs[ci * HW + iy * a.W + ix] : 0.0f;
-      }
-  float acc[EPC];
-#pragma unroll
-  for (int e = 0; e < EPC; ++e) acc[e] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-#pragma unroll
-    for (int q = 0; q < EPC / 4; ++q) {
-      const f32x4 w4 = *(const f32x4*)(hw + k * a.Cout + c0 + 4 * q);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[4 * q + e] = fmaf(w4[e], in[k], acc[4 * q + e]);
+  // block = one statistics slot of G pixels; thread = (pixel lane, 16-B chunk of couts)
+  const int HW = a.H * a.W, G = stat_slot_px(HW);
+  const int cq = a.Cout / EPC, plan = 256 / cq;
+  const int ch = threadIdx.x % cq, pl = threadIdx.x / cq, c0 = ch * EPC;
+  const long long pbase = (long long)blockIdx.x * G;
+  // the block's input window (3 channels, 1-pixel border) staged in LDS: whole rows
+  // when W <= G, else a G-wide row segment (host: G % W == 0 or W % G == 0)
+  const int img = (int)(pbase / HW), r0 = (int)(pbase - (long long)img * HW);
+  const int y0 = r0 / a.W, x0 = r0 - y0 * a.W;
+  const int TW = (a.W <= G ? a.W : G) + 2, TR = (a.W <= G ? G / a.W : 1) + 2;
+  float* tin = red + (size_t)plan * a.Cout * 2;  // [3][TR][TW]
+  {
+    const float* xs = a.x + (size_t)(img % a.x_img_mod) * 3 * HW;
+    for (int i = threadIdx.x; i < 3 * TR * TW; i += 256) {
+      const int ci = i / (TR * TW), r = i - ci * TR * TW, ty = r / TW, tx = r - ty * TW;
+      const int iy = y0 - 1 + ty, ix = x0 - 1 + tx;
+      tin[i] = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? xs[ci * HW + iy * a.W + ix] : 0.0f;
     }
   }
-  u32x4 w;
-  T* we = (T*)&w;
+  __syncthreads();
+  float ssum[EPC], ssq[EPC];
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(acc[e] + hw[a.Cout * 27 + c0 + e]);
-  *(u32x4*)((T*)a.out + (size_t)pix * a.Cout + c0) = w;
+  for (int e = 0; e < EPC; ++e) ssum[e] = ssq[e] = 0.f;
+  if (pl < plan) {
+    for (int p = pl; p < G; p += plan) {
+      const long long pix = pbase + p;
+      const int ly = a.W <= G ? p / a.W : 0, lx = a.W <= G ? p - ly * a.W : p;
+      float in[27];
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) in[ci * 9 + ky * 3 + kx] = tin[(ci * TR + ly + ky) * TW + lx + kx];
+      float acc[EPC];
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) acc[e] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 27; ++k) {
+#pragma unroll
+        for (int q = 0; q < EPC / 4; ++q) {
+          const f32x4 w4 = *(const f32x4*)(hw + k * a.Cout + c0 + 4 * q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[4 * q + e] = fmaf(w4[e], in[k], acc[4 * q + e]);
+        }
+      }
+      u32x4 w;
+      T* we = (T*)&w;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        we[e] = Elem<T>::to(acc[e] + hw[a.Cout * 27 + c0 + e]);
+        const float v = Elem<T>::tof(we[e]);  // statistics of the stored (rounded) tensor
+        ssum[e] += v;
+        ssq[e] += v * v;
+      }
+      *(u32x4*)((T*)a.out + (size_t)pix * a.Cout + c0) = w;
+    }
+  }
+  if (!a.stats) return;
+  // GroupNorm statistics slab of the head output: stats[slot][0|1][c] (fixed-order sums)
+  if (pl < plan) {
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      red[(pl * a.Cout + c0 + e) * 2] = ssum[e];
+      red[(pl * a.Cout + c0 + e) * 2 + 1] = ssq[e];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.Cout; c += 256) {
+    float s = 0.f, q = 0.f;
+    for (int l = 0; l < plan; ++l) {
+      s += red[(l * a.Cout + c) * 2];
+      q += red[(l * a.Cout + c) * 2 + 1];
+    }
+    a.stats[((size_t)blockIdx.x * 2) * a.Cout + c] = s;
+    a.stats[((size_t)blockIdx.x * 2 + 1) * a.Cout + c] = q;
+  }
 }
 
 template <typename T>
 hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   constexpr int EPC = 16 / (int)sizeof(T);
-  const long long total = (long long)a.n * a.H * a.W * (a.Cout / EPC);
-  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), a.Cout * 28 * sizeof(float), s,
-                     a);
+  const int HW = a.H * a.W, G = stat_slot_px(HW), cq = a.Cout / EPC;
+  if (a.Cout % EPC || cq > 256 || 256 % cq || HW % G || (G % a.W && a.W % G)) return hipErrorInvalidValue;
+  const int TW = (a.W <= G ? a.W : G) + 2, TR = (a.W <= G ? G / a.W : 1) + 2;
+  const size_t smem = ((size_t)a.Cout * 28 + (size_t)(256 / cq) * a.Cout * 2 + 3 * TR * TW) * sizeof(float);
+  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((long long)a.n * HW / G)), dim3(256), smem, s, a);
   return hipGetLastError();
 }
 template hipError_t launch_head<float>(const HeadArgs&, hipStream_t);
