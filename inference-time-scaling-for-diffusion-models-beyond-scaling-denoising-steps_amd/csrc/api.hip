@@ -34,6 +34,7 @@ hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hi
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
 bool conv_gn_eligible(int H, int W);
+hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
                         hipStream_t);
 }  // namespace itsd
@@ -76,7 +77,7 @@ struct Act {
   size_t stats = SIZE_MAX;  // ws offset of the channel-statistics slab (consumed by a GroupNorm), or none
 };
 
-enum OpKind { OP_GN, OP_CONV, OP_ATTN };
+enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF };
 
 struct Op {
   OpKind kind;
@@ -93,7 +94,7 @@ struct Op {
   // ATTN
   int S = 0, C = 0;
   int vt = -1, vt_from = 0;  // channel-major V buffer (conv: couts >= vt_from go there; attn: reads it)
-  int gnfuse = 0;            // CONV: GroupNorm(gamma, beta)+SiLU of the input fused into the conv
+  size_t coef = SIZE_MAX;    // GNCOEF: output; CONV: GroupNorm+SiLU coefficients of the input (fused conv)
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -267,20 +268,23 @@ struct Builder {
   int conv_layer(int s1, int s2, const std::string& name, int Cout, int ks, int stride, int pad, int ups, int Hout,
                  int Wout, int temb_col = -1, int resid = -1, const std::string& gn = "") {
     const int Cin = u->acts[s1].C + (s2 >= 0 ? u->acts[s2].C : 0);
-    size_t gg = 0, gb = 0;
-    if (!gn.empty()) {
-      gg = f32(gn + ".weight", Cin);
-      gb = f32(gn + ".bias", Cin);
+    size_t coef = SIZE_MAX;
+    if (!gn.empty()) {  // GN coefficient op feeding the fused conv
+      Op g;
+      g.kind = OP_GNCOEF;
+      g.src1 = s1; g.src2 = s2;
+      g.gamma = f32(gn + ".weight", Cin);
+      g.beta = f32(gn + ".bias", Cin);
+      g.coef = coef = ws_off;
+      ws_off = (ws_off + (size_t)u->nb_max * Cin * 2 * 4 + 255) & ~(size_t)255;
+      u->ops.push_back(g);
     }
     const float* W = get(name + ".weight", (int64_t)Cout * Cin * ks * ks);
     size_t wt = pack({W}, Cout, Cin, ks);
     size_t b = f32(name + ".bias", Cout);
     int dst = act(Hout, Wout, Cout);
     conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
-    if (!gn.empty()) {
-      Op& o = u->ops.back();
-      o.gnfuse = 1; o.gamma = gg; o.beta = gb;
-    }
+    u->ops.back().coef = coef;
     return dst;
   }
   // conv3x3(silu(GroupNorm(s1 ++ s2))) can run as one fused launch (conv3x3_gn_kernel)
@@ -477,7 +481,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   {
     std::vector<int> need;
     for (const Op& o : u->ops)
-      if (o.kind == OP_GN || (o.kind == OP_CONV && o.gnfuse)) {
+      if (o.kind == OP_GN || o.kind == OP_GNCOEF) {
         need.push_back(o.src1);
         if (o.src2 >= 0) need.push_back(o.src2);
       }
@@ -525,7 +529,18 @@ struct RunCtx {
 
 int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
   hipError_t e = hipSuccess;
-  if (o.kind == OP_GN) {
+  if (o.kind == OP_GNCOEF) {
+    GNArgs g{};
+    g.C1 = u->acts[o.src1].C;
+    g.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
+    g.HW = u->acts[o.src1].H * u->acts[o.src1].W;
+    g.gamma = u->wp(o.gamma);
+    g.beta = u->wp(o.beta);
+    g.eps = 1e-5f;
+    g.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
+    g.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    e = launch_gn_coef(g, c.nb, (float*)(u->ws + o.coef), s);
+  } else if (o.kind == OP_GN) {
     GNArgs a{};
     a.src1 = u->ap(o.src1);
     a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
@@ -579,14 +594,12 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
       a.vt_from = o.vt_from;
     }
     a.zins = o.zins;
-    if (o.gnfuse) {
+    a.dbg = itsd::g_conv_dbg;
+    if (o.coef != SIZE_MAX) {
       if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
           !conv_gn_eligible(in.H, in.W) || a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
         return fail(ITSD_ERR_INVALID, "internal: fused GroupNorm conv on an unsupported shape");
-      a.gn_gamma = u->wp(o.gamma);
-      a.gn_beta = u->wp(o.beta);
-      a.gn_st1 = (const float*)(u->ws + in.stats);
-      a.gn_st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+      a.gn_coef = (const float*)(u->ws + o.coef);
     }
     {  // the kernel moves 16-B chunks: every chunk must sit inside one source and one tap
       const int epc = u->bf16 ? 8 : 4;
@@ -725,6 +738,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "splitk")) {
     if (value < 0 || value > 64) return fail(ITSD_ERR_INVALID, "splitk in [0,64]");
     itsd::g_splitk = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "conv_dbg")) {  // measurements only (results are wrong when set): 1 no
+    // in-loop loads, 2 no MFMA, 4 no GN statistics, 8 no GN transform, 16 no epilogue
+    itsd::g_conv_dbg = value & 31;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
@@ -998,7 +1016,7 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
       for (int q = 0; q < 6; ++q) sh[q] = 0;
       if (i >= 1 && i - 1 < u->ops.size()) {
         const Op& o = u->ops[i - 1];
-        const Act& out = u->acts[o.dst];
+        const Act& out = u->acts[o.dst >= 0 ? o.dst : o.src1];
         const Act& in = u->acts[o.src1];
         sh[0] = n * out.H * out.W;
         sh[1] = o.kind == OP_CONV ? o.Cout : out.C;

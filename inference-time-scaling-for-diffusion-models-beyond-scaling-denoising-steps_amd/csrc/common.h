@@ -8,6 +8,7 @@ namespace itsd {
 
 extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_set_option)
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
+extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
@@ -84,12 +85,10 @@ struct ConvArgs {
   int vt_from;                       // (the V of a fused q|k|v projection, for the MFMA attention)
   float* splitk_ws;                  // split-K partial tiles (capacity splitk_cap floats) or null
   long long splitk_cap;
-  // fused GroupNorm+SiLU of the input (bf16 3x3, conv3x3_gn_kernel): gamma/beta [Cin] and the
-  // sources' statistics slabs; null gamma = plain conv
-  const float* gn_gamma;
-  const float* gn_beta;
-  const float* gn_st1;
-  const float* gn_st2;
+  // fused GroupNorm+SiLU of the input (bf16 3x3, conv3x3_gn_kernel): per-image channel
+  // coefficients coef[img][Cin/8][a0..a7, b0..b7] (gn_coef_kernel); null = plain conv
+  const float* gn_coef;
+  int dbg;                           // g_conv_dbg (measurements only)
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -24,6 +24,7 @@
 // Epilogue (shared, LDS-staged): + bias + temb_proj row (+ CFG cond_proj row) +
 // residual, coalesced 16-B stores, and the consumer GroupNorm's channel statistics.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -37,6 +38,7 @@ constexpr int EROW = 132;  // epilogue LDS row (floats)
 constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + statistics partials
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
 int g_fuse_gn = 1;
+int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 
@@ -131,45 +133,61 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     }
     return;
   }
-  const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+  // Additive vectors bias + temb row + CFG cond row per (image of the tile, cout),
+  // staged once in LDS (the statistics scratch R, free until the statistics pass).
+  // Host: the tile's pixels span whole images (HWo % 128 == 0) or 128 % HWo == 0.
+  float* addv = E + 128 * EROW;  // [<= 8 images][128]
+  const int img0 = tileP / HWo;
+  const int nimt = HWo >= 128 ? 1 : 128 / HWo;
+  {
+    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+    for (int it = tid; it < nimt * 128; it += NT) {
+      const int il = it >> 7, cl = it & 127, co = tileC + cl, img = img0 + il;
+      float v = 0.f;
+      if (co < a.Cout && (long long)img * HWo < a.M) {
+        v = a.bias[co];
+        if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
+        if (a.cemb) {
+          int lab = 0;
+          if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
+          v += a.cemb[(long long)lab * a.cemb_row_stride + co];
+        }
+      }
+      addv[it] = v;
+    }
+  }
   constexpr int CPR = 128 / EPC;  // 16-B output chunks per tile row
-  for (int it = tid; it < 128 * CPR; it += NT) {
-    const int pl = it / CPR, cl = (it - pl * CPR) * EPC;
-    const int p = tileP + pl, co = tileC + cl;
-    if (p >= a.M || co >= a.Cout) continue;
-    const int img = p / HWo;
+  const int cl = (tid % CPR) * EPC, co = tileC + cl;
+  const int RPI = NT / CPR;       // rows per pass
+  constexpr int MAXR = 128 * CPR / 256;
+  // residual rows first: all loads in flight before the first use
+  u32x4 rres[MAXR];
+  if (a.resid) {
+#pragma unroll
+    for (int k = 0; k < MAXR; ++k) {
+      const int pl = tid / CPR + k * RPI;
+      const int p = tileP + pl;
+      rres[k] = (pl < 128 && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + (size_t)p * a.Cout + co)
+                                                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < MAXR; ++k) {
+    const int pl = tid / CPR + k * RPI;
+    const int p = tileP + pl;
+    if (pl >= 128 || p >= a.M || co >= a.Cout) continue;
+    const float* av = addv + ((HWo >= 128 ? 0 : pl / HWo) << 7) + cl;
     float v[EPC];
 #pragma unroll
     for (int q = 0; q < EPC / 4; ++q) {
       const f32x4 e4 = *(const f32x4*)(E + pl * EROW + cl + 4 * q);
-      const f32x4 b4 = *(const f32x4*)(a.bias + co + 4 * q);
+      const f32x4 b4 = *(const f32x4*)(av + 4 * q);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
     }
-    if (a.temb) {
-      const float* tb = a.temb + trow + (long long)img * a.temb_img_stride + co;
-#pragma unroll
-      for (int q = 0; q < EPC / 4; ++q) {
-        const f32x4 t4 = *(const f32x4*)(tb + 4 * q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * q + e] += t4[e];
-      }
-    }
-    if (a.cemb) {
-      int lab = 0;
-      if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-      const float* cb = a.cemb + (long long)lab * a.cemb_row_stride + co;
-#pragma unroll
-      for (int q = 0; q < EPC / 4; ++q) {
-        const f32x4 c4 = *(const f32x4*)(cb + 4 * q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * q + e] += c4[e];
-      }
-    }
-    const size_t o = (size_t)p * a.Cout + co;
     if (a.resid) {
-      const u32x4 r = *(const u32x4*)((const T*)a.resid + o);
-      const T* re = (const T*)&r;
+      const T* re = (const T*)&rres[k];
 #pragma unroll
       for (int e = 0; e < EPC; ++e) v[e] += Elem<T>::tof(re[e]);
     }
@@ -177,7 +195,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     T* we = (T*)&w;
 #pragma unroll
     for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(v[e]);
-    *(u32x4*)((T*)a.out + o) = w;
+    *(u32x4*)((T*)a.out + (size_t)p * a.Cout + co) = w;
     if (a.stats) {
 #pragma unroll
       for (int q = 0; q < EPC / 4; ++q) {
@@ -433,9 +451,9 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
     else if (ahead == 1) wait_vmcnt<8>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    if (kc + NS - 1 < k1) issue(kc + NS - 1);
+    if (kc + NS - 1 < k1 && !(a.dbg & 1)) issue(kc + NS - 1);
     const char* A = smem + (kc % NS) * STAGE;
-    mma_stage<T>(A, A + TILEB, acc, wm, wn, rl, hh);
+    if (!(a.dbg & 2)) mma_stage<T>(A, A + TILEB, acc, wm, wn, rl, hh);
   }
   wait_vmcnt<0>();
   __syncthreads();
@@ -443,6 +461,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
     splitk_store(a, acc, z, S, bt, gridDim.x);
     return;
   }
+  if (a.dbg & 16) return;
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
@@ -584,59 +603,43 @@ __global__ __launch_bounds__(256, 2) void conv_igemm(ConvArgs a) {
 //     compiler's own vmcnt bookkeeping exact across the chunk loop.
 constexpr int GNC_ITEMS = 7;                    // halo pixels per thread (32 pixels x 8 chunks per pass)
 constexpr int GNC_HALO_ROWS = GNC_ITEMS * 32;  // 224: 32x32 6x34, 16x16 10x18, 8x8 2 x 10x10 (+ scratch rows)
-constexpr int GNC_SEGS = 4;                     // images per tile (group-statistics slots)
 constexpr int GNC_NS = 3;                       // weight ring depth
-constexpr int GNC_SMEM = GNC_HALO_ROWS * ROWB + GNC_NS * TILEB + GNC_SEGS * 32 * 2 * 4;
+constexpr int GNC_SMEM = GNC_HALO_ROWS * ROWB + GNC_NS * TILEB;
 static_assert(GNC_SMEM >= EPI_BYTES, "epilogue reuses the fused conv's LDS");
 static_assert(2 * GNC_SMEM <= 160 * 1024, "two blocks per CU");
 
-__device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// x*a + b then SiLU on two lanes of packed fp32 (v_pk_fma / v_pk_add / v_pk_mul), the
+// exp and reciprocal per element (bf16 output: fast reciprocal is below its rounding)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gn_silu2(f32x2 x, f32x2 sc, f32x2 sh) {
+  const f32x2 y = x * sc + sh;
+  f32x2 e;
+  e.x = __expf(-y.x);
+  e.y = __expf(-y.y);
+  const f32x2 d = e + 1.0f;
+  f32x2 r;
+  r.x = __builtin_amdgcn_rcpf(d.x);
+  r.y = __builtin_amdgcn_rcpf(d.y);
+  return y * r;
+}
 
+// NSEG = images per tile (1: 16x16 and larger, 2: 8x8).
+template <int NSEG>
 __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   typedef bf16_t T;
   __shared__ __attribute__((aligned(16))) char smem[GNC_SMEM];
   char* halo = smem;
   char* wring = smem + GNC_HALO_ROWS * ROWB;
-  float* gst = (float*)(wring + GNC_NS * TILEB);  // [seg][group][mean, rstd]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
   const TileId bt = tile_of_block();
   const int tileP = bt.x * CONV_BN, tileC = bt.y * CONV_BM;
   const int H = a.Hout, W = a.Wout, HW = H * W, W2 = W + 2;
-  const int Cin = a.C1 + a.C2, ncc = Cin / 64, nS = 9 * ncc, gsz = Cin / 32;
-  const int THs = min(H, 128 / W), segs = 128 / (THs * W), HS = (THs + 2) * W2, NH = segs * HS;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64, nS = 9 * ncc;
+  const int THs = min(H, 128 / W), HS = (THs + 2) * W2, NH = NSEG * HS;
   const int nimg = a.M / HW;
   const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
   const T* zero = zero_of_block<T>(a);
-
-  // ---- group statistics of the tile's images (fp64 over the slabs, fixed order)
-  {
-    const int pair = tid >> 1, half = tid & 1, seg = pair >> 5, g = pair & 31;
-    const int img = img0 + seg;
-    const int spi = HW / stat_slot_px(HW);
-    double s = 0.0, q = 0.0;
-    if (seg < segs && img < nimg) {
-      for (int k = half; k < gsz * spi; k += 2) {
-        const int c = g * gsz + k / spi;
-        const long long sl = (long long)img * spi + (k % spi);
-        const float* st;
-        int Cs, cs;
-        if (c < a.C1) { st = a.gn_st1; Cs = a.C1; cs = c; } else { st = a.gn_st2; Cs = a.C2; cs = c - a.C1; }
-        s += (double)st[(sl * 2) * Cs + cs];
-        q += (double)st[(sl * 2 + 1) * Cs + cs];
-      }
-    }
-    s += __shfl_xor(s, 1, 64);
-    q += __shfl_xor(q, 1, 64);
-    if (half == 0) {
-      const double E = (double)gsz * HW;
-      const double mean = s / E;
-      double var = q / E - mean * mean;
-      var = var > 0.0 ? var : 0.0;
-      gst[pair * 2] = (float)mean;
-      gst[pair * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
-    }
-  }
 
   // ---- per-lane addressing
   int hb[2];  // halo pixel of this lane's B columns at tap (0,0)
@@ -656,6 +659,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   }
   const int lch = tid & 7;
   int poff[GNC_ITEMS];  // input pixel (img*H + iy)*W + ix of halo row j, or -1 (padding / scratch row)
+  int hseg = 0;         // bit j: halo row j belongs to the tile's second image
 #pragma unroll
   for (int j = 0; j < GNC_ITEMS; ++j) {
     const int h = (tid >> 3) + 32 * j;
@@ -664,6 +668,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
       const int seg = h / HS, r = h - seg * HS, hy = r / W2, hx = r - hy * W2;
       const int img = img0 + seg, iy = y0 + hy - 1, ix = hx - 1;
       if (img < nimg && iy >= 0 && iy < H && ix >= 0 && ix < W) po = (img * H + iy) * W + ix;
+      hseg |= (seg & 1) << j;
     }
     poff[j] = po;
   }
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
     const int cc = s / 9, tap = s - cc * 9;
     const int k0 = tap * Cin + cc * 64;
     char* dst = wring + (s % GNC_NS) * TILEB;
-    const bool live = s < nS;
+    const bool live = s < nS && (s < 2 || !(a.dbg & 1));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const T* ga = (arow[q] >= 0 && live) ? (const T*)a.wt + (unsigned)(arow[q] + k0) : zero;
@@ -683,8 +688,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   };
   f32x16 acc[2][2];
   u32x4 hreg[GNC_ITEMS];
-  f32x4 gam[2], bet[2];
-  // 11 vector loads per lane: 7 halo chunks + gamma/beta of the lane's 8 channels
+  f32x4 cf0[4], cf1[4];  // per image of the tile: a[8], b[8] of this lane's 8 channels
+  // 7 + 4*NSEG vector loads per lane: the halo chunks and the lane's GN coefficients.
+  // Issued as inline asm: the compiler does not count the weight DMAs (LDS-direct
+  // loads) in its vmcnt scoreboard and would drain them with vmcnt(0) before the first
+  // use; the explicit counted waits of the tap loop retire these loads by tap 3.
+  constexpr int LPC = GNC_ITEMS + 4 * NSEG;
   auto load_chunk = [&](int cc) {
     const int ci0 = cc * 64;
     const bool s1 = ci0 < a.C1;
@@ -694,36 +703,41 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < GNC_ITEMS; ++j) {
       const T* p = src + (unsigned)(poff[j] * Cs + cs0);
-      hreg[j] = *(const u32x4*)(poff[j] >= 0 ? p : zero);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 ? p : zero) : "memory");
     }
-    const float* gp = a.gn_gamma + ci0 + lch * 8;
-    const float* bp = a.gn_beta + ci0 + lch * 8;
-    gam[0] = *(const f32x4*)gp;
-    gam[1] = *(const f32x4*)(gp + 4);
-    bet[0] = *(const f32x4*)bp;
-    bet[1] = *(const f32x4*)(bp + 4);
-  };
-  // y = silu(x*a + b), a = rstd*gamma, b = beta - mean*a; branch-free (scratch rows
-  // past the halo are written too) so every loaded register is consumed here
-  auto write_halo = [&](int cc) {
-    const int c0 = cc * 64 + lch * 8;
-    const int g0 = c0 / gsz, r0 = c0 - g0 * gsz;
-    int gi[8];
+    const f32x4* cp0 = (const f32x4*)(a.gn_coef + ((size_t)img0 * (Cin / 8) + cc * 8 + lch) * 16);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) gi[e] = g0 + (r0 + e >= gsz) + (r0 + e >= 2 * gsz) + (r0 + e >= 3 * gsz);
+    for (int q = 0; q < 4; ++q) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cf0[q]) : "v"(cp0 + q) : "memory");
+    if constexpr (NSEG == 2) {
+      const int img1 = min(img0 + 1, nimg - 1);
+      const f32x4* cp1 = (const f32x4*)(a.gn_coef + ((size_t)img1 * (Cin / 8) + cc * 8 + lch) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cf1[q]) : "v"(cp1 + q) : "memory");
+    }
+  };
+  // y = silu(x*a + b); branch-free (scratch rows past the halo are written too) so
+  // every loaded register is consumed here
+  auto write_halo = [&]() {
 #pragma unroll
     for (int j = 0; j < GNC_ITEMS; ++j) {
       const int h = (tid >> 3) + 32 * j;
-      const float* gs = gst + min(h / HS, GNC_SEGS - 1) * 64;
-      const T* xe = (const T*)&hreg[j];
-      u32x4 y;
-      T* ye = (T*)&y;
+      f32x4 c[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float2 mr = *(const float2*)(gs + 2 * gi[e]);
-        const float sc = mr.y * (e < 4 ? gam[0][e] : gam[1][e - 4]);
-        const float sh = (e < 4 ? bet[0][e] : bet[1][e - 4]) - mr.x * sc;
-        ye[e] = f2bf(silu_fast(bf2f(xe[e]) * sc + sh));
+      for (int q = 0; q < 4; ++q) c[q] = (NSEG == 2 && ((hseg >> j) & 1)) ? cf1[q] : cf0[q];
+      u32x4 y;
+      if (a.dbg & 8) {
+        y = hreg[j];
+      } else {
+        const uint32_t* xw = (const uint32_t*)&hreg[j];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
+          const f32x2 x = {__uint_as_float(xw[w] << 16), __uint_as_float(xw[w] & 0xffff0000u)};
+          const f32x4 av = c[w >> 1], bv = c[2 + (w >> 1)];
+          const f32x2 sc = (w & 1) ? f32x2{av[2], av[3]} : f32x2{av[0], av[1]};
+          const f32x2 sh = (w & 1) ? f32x2{bv[2], bv[3]} : f32x2{bv[0], bv[1]};
+          const f32x2 r = gn_silu2(x, sc, sh);
+          y[w] = (uint32_t)f2bf(r.x) | ((uint32_t)f2bf(r.y) << 16);
+        }
       }
       const bool pad = poff[j] < 0;
 #pragma unroll
@@ -732,6 +746,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
     }
   };
   auto mma_tap = [&](int s, int tap) {
+    if (a.dbg & 2) return;
     const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
     const char* A = wring + (s % GNC_NS) * TILEB;
 #pragma unroll
@@ -754,31 +769,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
 
   zero_acc(acc);
   load_chunk(0);
-  asm volatile("" ::: "memory");
   issue_w(0);
   issue_w(1);
+  wait_vmcnt<8>();  // the chunk-0 loads (older than the 8 weight DMAs)
+  write_halo();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // group statistics visible
-  write_halo(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  // The chunk loads and the halo rebuild run unconditionally (the last chunk re-stages
-  // itself, unused): the compiler then sees every loaded register consumed once per
-  // chunk and keeps its own vmcnt waits exact instead of draining the weight ring.
-  for (int cc = 0; cc < ncc; ++cc) {
-    const int s0 = cc * 9, cn = min(cc + 1, ncc - 1);
+  // One chunk = 9 taps. STAGE: also load + transform the next chunk's halo. The
+  // staging variant runs for every chunk but the last, so along each instantiation
+  // the loaded registers are consumed exactly once per iteration and the compiler's
+  // own vmcnt bookkeeping stays exact (no conservative drains of the weight ring).
+  auto run_chunk = [&](int cc, auto stage) {
+    constexpr bool ST = decltype(stage)::value;
+    const int s0 = cc * 9;
     // tap 0 (peeled): the next chunk's loads go out behind w(s0+2)
     wait_vmcnt<4>();
     __builtin_amdgcn_s_barrier();
     issue_w(s0 + 2);
-    asm volatile("" ::: "memory");
-    load_chunk(cn);
-    asm volatile("" ::: "memory");
+    if constexpr (ST) {
+      asm volatile("" ::: "memory");
+      load_chunk(cc + 1);
+      asm volatile("" ::: "memory");
+    }
     mma_tap(s0, 0);
     // taps 1-7 as a runtime loop; loads issued after stage s: w(s+1) (4), plus the
-    // next chunk's 11 while they sit in between (taps 1, 2)
+    // next chunk's LPC while they sit in between (taps 1, 2)
 #pragma unroll 1
     for (int tap = 1; tap < 8; ++tap) {
-      if (tap <= 2) wait_vmcnt<15>();
+      if (ST && tap <= 2) wait_vmcnt<4 + LPC>();
       else wait_vmcnt<4>();
       __builtin_amdgcn_s_barrier();
       issue_w(s0 + tap + 2);
@@ -789,14 +806,68 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     issue_w(s0 + 10);
     mma_tap(s0 + 8, 8);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading this chunk's halo
-    write_halo(cn);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
+    if constexpr (ST) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is done reading this chunk's halo
+      write_halo();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
+  run_chunk(ncc - 1, std::false_type{});
   wait_vmcnt<0>();
   __syncthreads();
+  if (a.dbg & 16) return;
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
+}
+
+// GroupNorm finalize for the fused conv (the statistics half of gn_apply_kernel): per
+// image the group mean / rstd in fp64 from the producers' slabs, then per channel
+// a = rstd*gamma, b = beta - mean*a as coef[img][C/8][a0..a7, b0..b7].
+__global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
+  __shared__ float gst[32][2];
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const int C = g.C1 + g.C2, gsz = C / 32;
+  const int spi = g.HW / stat_slot_px(g.HW), n = gsz * spi;
+  {
+    const int grp = tid >> 3, l8 = tid & 7;
+    double s = 0.0, q = 0.0;
+    for (int k = l8; k < n; k += 8) {
+      const int c = grp * gsz + k / spi;
+      const long long sl = (long long)img * spi + (k % spi);
+      const bool s1 = c < g.C1;
+      const float* st = s1 ? g.st1 : g.st2;
+      const int Cs = s1 ? g.C1 : g.C2, cs = s1 ? c : c - g.C1;
+      s += (double)st[(sl * 2) * Cs + cs];
+      q += (double)st[(sl * 2 + 1) * Cs + cs];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      q += __shfl_xor(q, o, 64);
+    }
+    if (l8 == 0) {
+      const double E = (double)gsz * g.HW;
+      const double mean = s / E;
+      double var = q / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      gst[grp][0] = (float)mean;
+      gst[grp][1] = (float)(1.0 / sqrt(var + (double)g.eps));
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int grp = c / gsz;
+    const float sc = gst[grp][1] * g.gamma[c];
+    float* o = coef + ((size_t)img * (C / 8) + c / 8) * 16 + (c & 7);
+    o[0] = sc;
+    o[8] = g.beta[c] - gst[grp][0] * sc;
+  }
+}
+
+hipError_t launch_gn_coef(const GNArgs& g, int n, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(gn_coef_kernel, dim3(n), dim3(256), 0, s, g, coef);
+  return hipGetLastError();
 }
 
 // Host-side eligibility of the fused kernel at an HxW level (the builder decides per conv).
@@ -805,15 +876,17 @@ bool conv_gn_eligible(int H, int W) {
   const int THs = std::min(H, 128 / W);
   if (THs * W == 0 || 128 % (THs * W) || H % THs) return false;
   const int segs = 128 / (THs * W);
-  return segs <= GNC_SEGS && segs * (THs + 2) * (W + 2) <= GNC_HALO_ROWS;
+  return segs <= 2 && segs * (THs + 2) * (W + 2) <= GNC_HALO_ROWS;
 }
 
 template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
-    if (a.gn_gamma) {
+    if (a.gn_coef) {
       dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
-      hipLaunchKernelGGL(conv3x3_gn_kernel, grid, dim3(256), 0, s, a);
+      const int THs = std::min(a.Hout, 128 / a.Wout), segs = 128 / (THs * a.Wout);
+      if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_kernel<1>, grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_gn_kernel<2>, grid, dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }

@@ -37,10 +37,12 @@ def main():
     if args.variants:
         from itsd import runtime as rt
         for rnd in range(3):
-            for v in args.variants.split(","):  # e.g. "2", "2s0" (variant 2, split-K off)
-                vv, _, sk = v.partition("s")
+            for v in args.variants.split(","):  # e.g. "2", "2s0" (split-K off), "2s1d1" (debug: no loads)
+                v0, _, dbg = v.partition("d")
+                vv, _, sk = v0.partition("s")
                 rt.set_option("conv_variant", int(vv))
                 rt.set_option("splitk", int(sk) if sk else 1)
+                rt.set_option("conv_dbg", int(dbg) if dbg else 0)
                 ops = nat.profile_ops(x, t)
                 conv = [o for o in ops if o["kind"] == "conv"]
                 by = defaultdict(lambda: [0.0, 0.0])
@@ -51,6 +53,7 @@ def main():
                       + " ".join(f"H{h}:{m:.3f}ms/{f / m / 1e9:.0f}TF" for h, (m, f) in sorted(by.items())))
         rt.set_option("conv_variant", 2)
         rt.set_option("splitk", 1)
+        rt.set_option("conv_dbg", 0)
     for _ in range(args.reps):
         ops = nat.profile_ops(x, t)
     tot = sum(o["ms"] for o in ops)
