@@ -87,6 +87,7 @@ struct Op {
   int silu = 0;
   // CONV
   int ksize = 3, stride = 1, pad = 1, upsample = 0, zins = 0;
+  int subpix = 0;  // upsample conv as 4 phase-wise 2x2 convs (conv.hip conv_pipe)
   size_t wt = 0, bias = 0;
   int Cout = 0, K = 0;
   int temb_col = -1;
@@ -228,6 +229,48 @@ struct Builder {
       return ar.add(b.data(), b.size() * 2);
     }
     return ar.add(tmp.data(), tmp.size() * 4);
+  }
+  // Nearest-x2 upsample + 3x3 conv (Model.py:123-125) as 4 sub-pixel phases: output
+  // (2i+py, 2j+px) sees input rows i+dy+py-1 (dy in {0,1}) with the 3x3 taps folded
+  // onto them: W'[ph][co][dy][dx][ci] = sum over ky in R(py,dy), kx in R(px,dx) of
+  // W[co][ci][ky][kx], R(0,0)={0}, R(0,1)={1,2}, R(1,0)={0,1}, R(1,1)={2}. Sums in fp64.
+  size_t pack_subpix(const float* W, int Cout, int Cin) {
+    static const int lo[2][2] = {{0, 1}, {0, 2}}, hi[2][2] = {{0, 2}, {1, 2}};  // [p][d] -> k range
+    const int K = 4 * Cin;
+    std::vector<float> tmp((size_t)4 * Cout * K, 0.f);
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      for (int co = 0; co < Cout; ++co)
+        for (int dy = 0; dy < 2; ++dy)
+          for (int dx = 0; dx < 2; ++dx)
+            for (int ci = 0; ci < Cin; ++ci) {
+              double acc = 0.0;
+              for (int ky = lo[py][dy]; ky <= hi[py][dy]; ++ky)
+                for (int kx = lo[px][dx]; kx <= hi[px][dx]; ++kx)
+                  acc += W ? (double)W[(((size_t)co * Cin + ci) * 3 + ky) * 3 + kx] : 0.0;
+              tmp[((size_t)ph * Cout + co) * K + (dy * 2 + dx) * Cin + ci] = (float)acc;
+            }
+    }
+    if (u->bf16) {
+      std::vector<uint16_t> b(tmp.size());
+      for (size_t i = 0; i < tmp.size(); ++i) b[i] = host_f2bf(tmp[i]);
+      return ar.add(b.data(), b.size() * 2);
+    }
+    return ar.add(tmp.data(), tmp.size() * 4);
+  }
+  int upconv(int s1, const std::string& name, int Cout, int Hout) {
+    const Act& A = u->acts[s1];
+    const int Cin = A.C, epc = u->bf16 ? 8 : 4;
+    if ((A.H * A.W) % 128 || Cin % (8 * epc))  // sub-pixel tiles must stay inside one image
+      return conv_layer(s1, -1, name, Cout, 3, 1, 1, 1, Hout, Hout);
+    const float* W = get(name + ".weight", (int64_t)Cout * Cin * 9);
+    size_t wt = pack_subpix(W, Cout, Cin);
+    size_t b = f32(name + ".bias", Cout);
+    int dst = act(Hout, Hout, Cout);
+    conv(s1, -1, dst, wt, b, Cout, 3, 1, 1, 1);
+    Op& o = u->ops.back();
+    o.subpix = 1;
+    return dst;
   }
   size_t concat_f32(const std::vector<const float*>& parts, int n) {
     std::vector<float> tmp((size_t)n * parts.size(), 0.f);
@@ -425,7 +468,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
       const std::string p = P("upblocks", nup++);
       const int Hc = b.u->acts[cur].H;
       if (!u->cfg) {
-        cur = b.conv_layer(cur, -1, p + ".main", now, 3, 1, 1, 1, 2 * Hc, 2 * Hc);
+        cur = b.upconv(cur, p + ".main", now, 2 * Hc);
       } else {  // ConvTranspose2d(5, 2, 2, 1) then Conv 3x3, ModelCondition.py:83-85
         const float* Wt = b.get(p + ".t.weight", (int64_t)now * now * 25);
         size_t wt = b.pack({Wt}, now, now, 5, true);
@@ -595,6 +638,13 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     }
     a.zins = o.zins;
     a.dbg = itsd::g_conv_dbg;
+    if (o.subpix) {  // input-grid GEMM with 2x2 taps per phase (conv.hip)
+      a.subpix = 1;
+      a.Hout = in.H; a.Wout = in.W;
+      a.M = c.nb * in.H * in.W;
+      a.ksize = 2; a.pad = 0; a.upsample = 0;
+      a.K = 4 * (a.C1 + a.C2);
+    }
     if (o.coef != SIZE_MAX) {
       if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
           !conv_gn_eligible(in.H, in.W) || a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
@@ -621,9 +671,9 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
 }
 
 double op_flops(const itsd_unet* u, const Op& o, int nb) {
-  if (o.kind == OP_CONV) {
+  if (o.kind == OP_CONV) {  // executed MFMA work (sub-pixel upsample convs: 4 of the 9 taps)
     const Act& out = u->acts[o.dst];
-    return 2.0 * nb * out.H * out.W * (double)o.Cout * o.K;
+    return 2.0 * nb * out.H * out.W * (double)o.Cout * (o.subpix ? o.K * 4 / 9 : o.K);
   }
   if (o.kind == OP_ATTN) return 2.0 * 2.0 * nb * (double)o.S * o.S * o.C;
   return 0.0;

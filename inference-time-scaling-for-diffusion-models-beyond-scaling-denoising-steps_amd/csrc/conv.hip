@@ -94,27 +94,46 @@ __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (
 //    GroupNorm statistics of the consumer (Model.py:171,180), written as a
 //    deterministic partial slab stats[slot][2][Cout] (no atomics).
 template <typename T>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int tileP,
-                                              int tileC) {
-  // waves 0..3 own the 128x128 accumulator tile; a block may have more threads (NT)
-  constexpr int EPC = 16 / (int)sizeof(T);
-  const int NT = blockDim.x;
+__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
+
+// accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
+__device__ __forceinline__ void acc_to_E(f32x16 (&acc)[2][2], float* E, int pbase) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid >> 1) & 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        *(f32x4*)(E + (pbase + wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
+      }
+}
+
+template <typename T>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int tileP,
+                                              int tileC, int phase = -1) {
+  if (threadIdx.x < 256) acc_to_E(acc, (float*)smem, 0);
+  __syncthreads();
+  epilogue_from_E<T>(a, smem, tileP, tileC, phase);
+}
+
+// E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
+// and the consumer GroupNorm's statistics slab.
+template <typename T>
+__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const int NT = blockDim.x;
+  const int tid = threadIdx.x;
   const int HWo = a.Hout * a.Wout;
   float* E = (float*)smem;
-  if (tid < 256) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
-        }
-  }
-  __syncthreads();
+  // output row of tile-space pixel p (sub-pixel phase convs write a 2x grid)
+  auto orow = [&](int p) -> size_t {
+    if (phase < 0) return (size_t)p;
+    const int img = p / HWo, rem = p - img * HWo, i = rem / a.Wout, j = rem - i * a.Wout;
+    return ((size_t)img * 2 * a.Hout + 2 * i + (phase >> 1)) * (2 * a.Wout) + 2 * j + (phase & 1);
+  };
   if (a.vt_out && tileC >= a.vt_from) {
     // channel-major store of this (whole-V) tile: vt[img][c][pixel], 16-B chunks of
     // consecutive pixels of one image (host: HWo % EPC == 0, vt_from % 128 == 0); + bias only.
@@ -167,7 +186,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     for (int k = 0; k < MAXR; ++k) {
       const int pl = tid / CPR + k * RPI;
       const int p = tileP + pl;
-      rres[k] = (pl < 128 && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + (size_t)p * a.Cout + co)
+      rres[k] = (pl < 128 && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + orow(p) * a.Cout + co)
                                                       : u32x4{0u, 0u, 0u, 0u};
     }
   }
@@ -195,7 +214,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
     T* we = (T*)&w;
 #pragma unroll
     for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(v[e]);
-    *(u32x4*)((T*)a.out + (size_t)p * a.Cout + co) = w;
+    *(u32x4*)((T*)a.out + orow(p) * a.Cout + co) = w;
     if (a.stats) {
 #pragma unroll
       for (int q = 0; q < EPC / 4; ++q) {
@@ -239,7 +258,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
           sum += R[(g * 2) * 128 + cl];
           sq += R[(g * 2 + 1) * 128 + cl];
         }
-        const long long slot = p0 / Gt;
+        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * (HWo / 128) + phase * (HWo / 128) + (p0 % HWo) / 128;
         a.stats[(slot * 2) * a.Cout + co] = sum;
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
@@ -254,7 +273,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
           sum += v;
           sq = fmaf(v, v, sq);
         }
-        const long long slot = p0 / Gt;
+        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * (HWo / 128) + phase * (HWo / 128) + (p0 % HWo) / 128;
         a.stats[(slot * 2) * a.Cout + co] = sum;
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
@@ -358,6 +377,10 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   const int cpt = Cin / BK;  // K-chunks per tap
   const int nK = a.ksize * a.ksize * cpt;
   const int HWo = a.Hout * a.Wout;
+  // sub-pixel phase (upsample convs): 2x2 taps at input offsets (dy + py - 1, dx + px - 1)
+  const int phase = a.subpix ? bt.z : -1;
+  const int padY = a.subpix ? 1 - (phase >> 1) : a.pad, padX = a.subpix ? 1 - (phase & 1) : a.pad;
+  const T* wbase = (const T*)a.wt + (a.subpix ? (size_t)phase * a.Cout * a.K : 0);
   const int Hv = a.upsample ? 2 * a.Hin : (a.zins ? 2 * a.Hin - 1 : a.Hin);
   const int Wv = a.upsample ? 2 * a.Win : (a.zins ? 2 * a.Win - 1 : a.Win);
   const T* zero = zero_of_block<T>(a);
@@ -379,15 +402,15 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
     const int r = 8 * (4 * wid + q) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int co = tileC + r;
-    arow[q] = (const T*)a.wt + (size_t)(co < a.Cout ? co : 0) * a.K + c * EPC;
+    arow[q] = wbase + (size_t)(co < a.Cout ? co : 0) * a.K + c * EPC;
     if (co >= a.Cout) arow[q] = nullptr;
     const int p = tileP + r;
     const bool pv = p < a.M;
     const int img = p / HWo;
     const int rem = p - img * HWo;
     const int oy = rem / a.Wout;
-    const int iy0 = oy * a.stride - a.pad;
-    const int ix0 = (rem - oy * a.Wout) * a.stride - a.pad;
+    const int iy0 = oy * a.stride - padY;
+    const int ix0 = (rem - oy * a.Wout) * a.stride - padX;
     const int pl = (img * a.Hin + iy0) * a.Win + ix0;
     pix1[q] = pl * a.C1 + c * EPC;
     pix2[q] = pl * a.C2 + c * EPC;
@@ -438,8 +461,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
 
   f32x16 acc[2][2];
   zero_acc(acc);
-  // split-K: slice z of gridDim.z covers K-stages [k0, k1)
-  const int S = gridDim.z, z = bt.z;
+  // split-K: slice z of gridDim.z covers K-stages [k0, k1) (sub-pixel launches use z as phase)
+  const int S = a.subpix ? 1 : gridDim.z, z = a.subpix ? 0 : bt.z;
   const int k0 = (int)((long long)nK * z / S), k1 = (int)((long long)nK * (z + 1) / S);
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -462,7 +485,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
     return;
   }
   if (a.dbg & 16) return;
-  conv_epilogue<T>(a, acc, smem, tileP, tileC);
+  conv_epilogue<T>(a, acc, smem, tileP, tileC, phase);
 }
 
 template <typename T>
@@ -896,6 +919,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   const bool pipe = a.zero && Cin % BK == 0 && a.C1 % BK == 0 && a.K == a.ksize * a.ksize * Cin;
   const int v = g_conv_variant;
   const bool lin = !(a.upsample | a.zins);
+  if (a.subpix) {
+    if (!pipe || !lin || a.ksize != 2 || (a.Hout * a.Wout) % 128) return hipErrorInvalidValue;
+    grid.z = 4;
+    hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (pipe && v == 2 && a.splitk_ws && g_splitk) {
     // under-filled grids (the 8x8 / 4x4 levels): split K so that >= ~2 blocks per CU exist,
     // keeping >= 8 K-stages per slice
