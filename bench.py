@@ -119,25 +119,48 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    # conv-kernel census: one forward at the bench batch with HIP events around every launch
+    # Roofline of the dominant kernel: one census forward at the bench batch with HIP events
+    # around every launch on the UNet's stream (itsd_profile_ops). Dominant = the conv kind
+    # with the most time: "convgn" = conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3),
+    # "conv" = conv_pipe (+ split-K epilogue). FLOPs are the MFMA work each launch executes.
     roof = None
     if rank == 0:
         x = torch.randn(n_local, 3, 32, 32, device=dev)
         t = torch.full((n_local,), 500, dtype=torch.int32, device=dev)
         nat = net.native(n_local)
         for _ in range(2):
-            cen = nat.profile_forward(x, t)
-        avg_ms = cen["conv_ms"] / cen["conv_launches"]
-        flops_per_launch = cen["conv_flops"] / cen["conv_launches"]
-        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+            ops = nat.profile_ops(x, t)
+        agg = {}
+        for o in ops:
+            if o["kind"] in ("conv", "convgn"):
+                g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
+                g[0] += 1
+                g[1] += o["ms"]
+                g[2] += o["flops"]
+        kind = max(agg, key=lambda k: agg[k][1])
+        n_l, ms_sum, fl_sum = agg[kind]
+        avg_ms = ms_sum / n_l
+        achieved = fl_sum / (ms_sum * 1e-3) / 1e12
         peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
+        total_ms = sum(o["ms"] for o in ops)
+        conv_ms = sum(v[1] for v in agg.values())
+        conv_fl = sum(v[2] for v in agg.values())
+        names = {"convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3)",
+                 "conv": "conv_pipe (implicit-GEMM conv)"}
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kind}.json")
+        if os.path.exists(tfile) and args.precision == "bf16" and n_local == 256:
+            with open(tfile) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": "conv_pipe<bf16> (all implicit-GEMM conv launches of a forward)" if args.precision == "bf16" else "conv_pipe<f32>",
-                "avg_launch_ms": round(avg_ms, 4), "launches_per_forward": cen["conv_launches"],
-                "conv_share_of_forward": round(cen["conv_ms"] / cen["total_ms"], 4),
-                "forward_ms": round(cen["total_ms"], 3),
-                "forward_tflops": round(flops_per_image(a) * n_local / (cen["total_ms"] * 1e-3) / 1e12, 2)}
+                "frac": round(achieved / peak, 4), "traffic": traffic,
+                "kernel": names[kind], "launches_per_forward": n_l, "avg_launch_ms": round(avg_ms, 4),
+                "flops_per_launch": fl_sum / n_l,
+                "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
+                "all_conv_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+                "conv_share_of_forward": round(conv_ms / total_ms, 4),
+                "forward_ms": round(total_ms, 3),
+                "forward_tflops_algorithmic": round(flops_per_image(a) * n_local / (total_ms * 1e-3) / 1e12, 2)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -78,6 +78,7 @@ struct Act {
 };
 
 enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF };
+constexpr int kCensusConvGN = 4;  // census kind of a fused GroupNorm+SiLU conv (conv3x3_gn_kernel)
 
 struct Op {
   OpKind kind;
@@ -706,7 +707,10 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
-  for (const Op& o : u->ops) CHK(mark((int)o.kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
+  // census kinds: OpKind, and kCensusConvGN for the fused GroupNorm+SiLU convs
+  for (const Op& o : u->ops)
+    CHK(mark(o.kind == OP_CONV && o.coef != SIZE_MAX ? kCensusConvGN : (int)o.kind, op_flops(u, o, c.nb),
+             [&]() { return launch_op(u, o, c, s); }));
   // tail GN + conv (+ sampler update)
   Op g;
   g.kind = OP_GN;
@@ -1014,7 +1018,7 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
     float ms = 0.f;
     if (r == ITSD_OK && e == hipSuccess) hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
     tm += ms;
-    if (kinds[i] == OP_CONV) { cm += ms; cf += fl[i]; ++cl; }
+    if (kinds[i] == OP_CONV || kinds[i] == kCensusConvGN) { cm += ms; cf += fl[i]; ++cl; }
     hipEventDestroy(evs[i].first);
     hipEventDestroy(evs[i].second);
   }

@@ -44,7 +44,7 @@ def main():
                 rt.set_option("splitk", int(sk) if sk else 1)
                 rt.set_option("conv_dbg", int(dbg) if dbg else 0)
                 ops = nat.profile_ops(x, t)
-                conv = [o for o in ops if o["kind"] == "conv"]
+                conv = [o for o in ops if o["kind"] in ("conv", "convgn")]
                 by = defaultdict(lambda: [0.0, 0.0])
                 for o in conv:
                     by[o["H"]][0] += o["ms"]
@@ -63,7 +63,7 @@ def main():
         tf = o["flops"] / (o["ms"] * 1e-3) / 1e12 if o["ms"] > 0 and o["flops"] > 0 else 0.0
         print(f"{i:3d} {o['kind']:5} {o['M']:7d} {o['N']:5d} {o['K']:5d} {o['H']:3d} {o['ks']:2d} {o['stride_up']:3d} "
               f"{o['ms']:8.4f} {tf:7.1f}")
-        key = o["kind"] if o["kind"] != "conv" else f"conv H{o['H']}"
+        key = o["kind"] if o["kind"] not in ("conv", "convgn") else f"{o['kind']} H{o['H']}"
         agg[key][0] += 1
         agg[key][1] += o["ms"]
         agg[key][2] += o["flops"]

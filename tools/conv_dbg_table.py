@@ -26,7 +26,7 @@ for d in DBG:
 rt.set_option("conv_dbg", 0)
 print(f"{'#':>3} {'kind':5} {'M':>7} {'N':>5} {'K':>5} {'H':>3} {'ks':>2} " + " ".join(f"{'d%d' % d:>7}" for d in DBG))
 for i, o in enumerate(res[0]):
-    if o["kind"] != "conv":
+    if o["kind"] not in ("conv", "convgn"):
         continue
     print(f"{i:3d} {o['kind']:5} {o['M']:7d} {o['N']:5d} {o['K']:5d} {o['H']:3d} {o['ks']:2d} " +
           " ".join(f"{res[d][i]['ms']*1e3:7.1f}" for d in DBG))
