@@ -17,6 +17,8 @@
  *   itsd_verify                  <- OracleVerifier / SelfSupervisedVerifier /
  *                                   AestheticPredictor .score (search/verifier.py:45-66,
  *                                   223-248, 262-287), batched per candidate
+ *   itsd_attention               <- AttnBlock core softmax(q k^T C^-0.5) v
+ *                                   (Diffusion/Model.py:152-161, ModelCondition.py:105-115)
  *   itsd_profile_forward         <- (no reference counterpart) per-kernel census used
  *                                   by bench.py for the roofline line
  *
@@ -113,6 +115,14 @@ int itsd_noise(float* out, const float* pivot, int n_cand, int64_t per_cand, flo
 /* scores[c] = verifier(images[c*b:(c+1)*b]) for c < n_cand; images NCHW fp32. */
 int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w,
                 double* scores, void* stream);
+
+/* AttnBlock core on n images of S tokens, width C (single head):
+ *   out[i][s][:] = softmax_j(q_s . k_j * C^-0.5) v_j
+ * qkv: [n][S][3C] (q | k | v per token, the fused projection the UNet produces);
+ * precision ITSD_PREC_FP32: fp32 tensors; ITSD_PREC_BF16: bf16 tensors and vt, the
+ * channel-major V [n][C][S] (the MFMA kernels read V^T; S <= 256: whole-row kernel,
+ * S > 256: flash kernel, C in {64,128,256}), out [n][S][C]. */
+int itsd_attention(const void* qkv, const void* vt, void* out, int n, int S, int C, int precision, void* stream);
 
 /* Census of one forward at batch n (synchronous): runs the op program eagerly with
  * HIP events around every launch. Outputs (any may be NULL):

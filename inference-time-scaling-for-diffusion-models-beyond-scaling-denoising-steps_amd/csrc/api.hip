@@ -26,6 +26,7 @@ namespace itsd {
 template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
 template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
 template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
+bool attn_flash_ok(int S, int C);
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
 hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
@@ -377,7 +378,8 @@ struct Builder {
       // MFMA attention (bf16): V goes channel-major to its own buffer from the conv epilogue
       const int S = H * W;
       int vt = -1;
-      if (u->bf16 && S <= 256 && S % 16 == 0 && out_ch % 64 == 0) {
+      // (S <= 256: whole-row MFMA kernel; longer sequences: flash kernel, C <= 256)
+      if (u->bf16 && S % 16 == 0 && out_ch % 64 == 0 && (S <= 256 || attn_flash_ok(S, out_ch))) {
         vt = act(out_ch, S, 1);
         u->ops.back().vt = vt;
         u->ops.back().vt_from = 2 * out_ch;
@@ -979,6 +981,27 @@ int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, 
   if (kind == ITSD_VERIFY_SELFSUP && (c * 64 > 192 || h % 8 || w % 8 || b > 64))
     return fail(ITSD_ERR_INVALID, "selfsup verifier needs c<=3, h,w divisible by 8, b<=64");
   HIPCHK(launch_verify(kind, images, n_cand, b, c, h, w, scores, (hipStream_t)stream));
+  return ITSD_OK;
+}
+
+int itsd_attention(const void* qkv, const void* vt, void* out, int n, int S, int C, int precision, void* stream) {
+  if (!qkv || !out || n < 1 || S < 1 || C < 1) return fail(ITSD_ERR_INVALID, "bad attention arguments");
+  if (precision != ITSD_PREC_FP32 && precision != ITSD_PREC_BF16) return fail(ITSD_ERR_INVALID, "precision");
+  AttnArgs a{};
+  a.qkv = qkv; a.out = out; a.S = S; a.C = C;
+  a.scale = (float)std::pow((double)C, -0.5);
+  if (precision == ITSD_PREC_BF16) {
+    if (C % 8) return fail(ITSD_ERR_INVALID, "C must be a multiple of 8");
+    if (vt) {
+      if (S % 16 || C % 64 || (S > 256 && !attn_flash_ok(S, C)))
+        return fail(ITSD_ERR_INVALID, "MFMA attention needs S % 16 == 0, C % 64 == 0 (S > 256: C in {64,128,256})");
+      a.vt = vt;
+    }
+    HIPCHK(launch_attn<bf16_t>(a, n, (hipStream_t)stream));
+  } else {
+    if (C % 4) return fail(ITSD_ERR_INVALID, "C must be a multiple of 4");
+    HIPCHK(launch_attn<float>(a, n, (hipStream_t)stream));
+  }
   return ITSD_OK;
 }
 

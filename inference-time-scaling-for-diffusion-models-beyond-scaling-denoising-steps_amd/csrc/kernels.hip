@@ -236,6 +236,112 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
   }
 }
 
+// Flash-style MFMA attention for long sequences (S > 256: the CFG UNet's 32x32 level,
+// S = 1024, C = 128, ModelCondition.py:98-118; Arch A at 64/256 px). No S x S tile is
+// materialised: each wave owns 32 queries and streams 32-key tiles with an online softmax.
+//  - scores are computed transposed, s^T = K q^T (A = 32 keys x 16 ch from the q|k|v rows,
+//    B = q^T), so every lane holds 16 keys of ONE query: the row max / row sum is a
+//    register reduction plus one xor-32 shuffle, and the rescale of O is one factor/lane;
+//  - O^T = V^T P^T with P^T straight from the score registers (bf16): the MFMA B operand
+//    of lane (query, hi) is its 8 score registers r = 8j..8j+7, i.e. keys
+//    {16j+4hi+0..3, 16j+8+4hi+0..3}; the A operand (V^T, channel-major from the qkv conv
+//    epilogue) is read with the same key permutation (two 8-B loads per lane), so the
+//    contraction over keys is exact without any register shuffle.
+// CB = C / 32 channel blocks (C <= 256: q fragment and O accumulators stay in registers).
+template <int CB>
+__global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
+  constexpr int C = CB * 32, C3 = 3 * C, QS = C / 16;
+  const int S = a.S;
+  const int img = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, rl = lane & 31, hh = lane >> 5;
+  const int q = blockIdx.x * 128 + wid * 32 + rl;
+  const bool qv = q < S;
+  const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
+  const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 qf[QS];
+  {
+    const bf16_t* qp = base + (size_t)(qv ? q : 0) * C3 + 8 * hh;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) qf[i] = qv ? *(const bf16x8*)(qp + 16 * i) : z8;
+  }
+  f32x16 o[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[cb][r] = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;  // softmax via exp2
+  float m = -INFINITY, l = 0.f;
+  for (int kt = 0; kt < S; kt += 32) {
+    const int key = kt + rl;
+    const bool kv = key < S;
+    const bf16_t* kp = base + (size_t)(kv ? key : 0) * C3 + C + 8 * hh;
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      const bf16x8 kf = kv ? *(const bf16x8*)(kp + 16 * i) : z8;
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[i], s, 0, 0, 0);
+    }
+    // s[r] = score(query rl, key kt + (r&3) + 8(r>>2) + 4hh) (unscaled)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      s[r] = kk < S ? s[r] * sl2 : -INFINITY;
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = exp2f(s[r] - mn);
+      rs += s[r];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf16x8 bp;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bp[i] = (short)f2bf(s[8 * j + i]);
+      const int k0 = kt + 16 * j + 4 * hh;  // keys k0..k0+3 and k0+8..k0+11 (S % 8 == 0)
+      const bool v0 = k0 < S, v1 = k0 + 8 < S;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        const bf16_t* vp = vt + (size_t)(cb * 32 + rl) * S;
+        uint2 lo = v0 ? *(const uint2*)(vp + k0) : make_uint2(0, 0);
+        uint2 hi = v1 ? *(const uint2*)(vp + k0 + 8) : make_uint2(0, 0);
+        u32x4 w = {lo.x, lo.y, hi.x, hi.y};
+        o[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), bp, o[cb], 0, 0, 0);
+      }
+    }
+  }
+  if (!qv) return;
+  const float inv = 1.0f / l;
+  bf16_t* out = (bf16_t*)a.out + ((size_t)img * S + q) * C;
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = cb * 32 + 8 * g + 4 * hh;
+      uint2 w2;
+      w2.x = (uint32_t)f2bf(o[cb][4 * g] * inv) | ((uint32_t)f2bf(o[cb][4 * g + 1] * inv) << 16);
+      w2.y = (uint32_t)f2bf(o[cb][4 * g + 2] * inv) | ((uint32_t)f2bf(o[cb][4 * g + 3] * inv) << 16);
+      *(uint2*)(out + c) = w2;
+    }
+}
+
+bool attn_flash_ok(int S, int C) { return S % 8 == 0 && (C == 64 || C == 128 || C == 256); }
+
 size_t attn_mfma_smem(int S) {
   const int Sp = (S + 31) & ~31;
   return (size_t)64 * (Sp + 4) * 4 + (size_t)64 * (Sp * 2 + 16);
@@ -244,6 +350,14 @@ size_t attn_mfma_smem(int S) {
 template <typename T>
 hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
+    if (a.vt && a.S > 256) {
+      if (!attn_flash_ok(a.S, a.C)) return hipErrorInvalidValue;
+      const dim3 grid((a.S + 127) / 128, n);
+      if (a.C == 64) hipLaunchKernelGGL(attn_flash_kernel<2>, grid, dim3(256), 0, s, a);
+      else if (a.C == 128) hipLaunchKernelGGL(attn_flash_kernel<4>, grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL(attn_flash_kernel<8>, grid, dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
     if (a.vt) {
       static bool attr = false;
       const size_t sm = attn_mfma_smem(a.S);

@@ -57,6 +57,8 @@ _SIGS = {
                    ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p],
     "itsd_verify": [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                     ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p],
+    "itsd_attention": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_int, ctypes.c_void_p],
     "itsd_profile_forward": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double), ctypes.c_void_p],
@@ -217,3 +219,18 @@ def verify(kind: int, images: torch.Tensor, n_cand: int) -> torch.Tensor:
     check(lib().itsd_verify(int(kind), images.data_ptr(), int(n_cand), N // n_cand, C, H, W, scores.data_ptr(),
                             stream_ptr(images.device)))
     return scores
+
+
+def attention(qkv: torch.Tensor, vt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """AttnBlock core (Model.py:152-161) on qkv [n][S][3C]; bf16 inputs take the MFMA
+    kernels and need vt = V channel-major [n][C][S]. Returns out [n][S][C]."""
+    assert qkv.is_cuda and qkv.is_contiguous() and qkv.dim() == 3 and qkv.shape[2] % 3 == 0
+    n, S, C3 = qkv.shape
+    C = C3 // 3
+    prec = PREC_BF16 if qkv.dtype == torch.bfloat16 else PREC_FP32
+    assert prec == PREC_BF16 or qkv.dtype == torch.float32
+    if vt is not None:
+        assert vt.dtype == qkv.dtype and vt.is_contiguous() and tuple(vt.shape) == (n, C, S)
+    out = torch.empty(n, S, C, dtype=qkv.dtype, device=qkv.device)
+    check(lib().itsd_attention(qkv.data_ptr(), _ptr(vt), out.data_ptr(), n, S, C, prec, stream_ptr(qkv.device)))
+    return out

@@ -15,7 +15,9 @@ import torch
 
 from conftest import golden
 from oracle import ref_cpu as R
-from itsd.arch import ARCH_A, ARCH_TINY, ARCH_TINY_CFG
+import dataclasses
+
+from itsd.arch import ARCH_A, ARCH_C, ARCH_TINY, ARCH_TINY_CFG
 from itsd.diffusion import CondGaussianDiffusionSampler, GaussianDiffusionSampler, reference_noise_plan
 from itsd.model import CondUNet, UNet
 from itsd.search import SearchEngine
@@ -32,9 +34,10 @@ REL_L2_BF16 = 2e-2
 
 def _net(a, precision="fp32", seed=0):
     if a.cfg:
-        net = CondUNet(a.T, a.num_labels, a.ch, a.ch_mult, a.num_res_blocks, 0.0, precision=precision)
+        net = CondUNet(a.T, a.num_labels, a.ch, a.ch_mult, a.num_res_blocks, 0.0, img_size=a.img_size,
+                       precision=precision)
     else:
-        net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=precision)
+        net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=a.img_size, precision=precision)
     net.load_state_dict(synthetic_state_dict(a, seed))
     return net.to("cuda:0")
 
@@ -80,6 +83,27 @@ def test_forward_bf16_archA_vs_oracle(n):
     with torch.no_grad():
         ref = _oracle(a, sd)(x, t)
     assert _rel_l2(eps, ref) < REL_L2_BF16
+
+
+ARCH_A64 = dataclasses.replace(ARCH_A, img_size=64)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("arch,fix", [(ARCH_C, "archC_eps"), (ARCH_A64, "archA64_eps")])
+def test_forward_full_configs_vs_reference(arch, fix, precision):
+    """C3 (CFG UNet, flash attention at S = 1024 in bf16) and C4 (Arch A at 64 px)
+    against reference outputs: fp32 max-abs, bf16 relative L2."""
+    g = golden(fix)
+    net = _net(arch, precision)
+    args = [torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["t"]).cuda()]
+    if arch.cfg:
+        args.append(torch.from_numpy(g["labels"]).cuda())
+    eps = net(*args).cpu()
+    ref = torch.from_numpy(g["eps"])
+    if precision == "fp32":
+        np.testing.assert_allclose(eps.numpy(), ref.numpy(), atol=EPS_TOL_FP32, rtol=0)
+    else:
+        assert _rel_l2(eps, ref) < REL_L2_BF16
 
 
 def test_trajectory_tiny_fp32_vs_reference():
@@ -216,3 +240,34 @@ def test_engine_random_search_full_T_archA_bf16():
     assert torch.isfinite(sc).all()
     assert best_score == sc.max().item() and info["best_index"] == int(torch.argmax(sc))
     assert best_noise.shape == (1, 3, 32, 32)
+
+
+def _attn_ref(qkv):
+    """Plain PyTorch fp32 AttnBlock core (Model.py:152-161)."""
+    q, k, v = qkv.float().chunk(3, dim=2)
+    w = torch.bmm(q, k.transpose(1, 2)) * (q.shape[2] ** -0.5)
+    return torch.bmm(torch.softmax(w, dim=-1), v)
+
+
+@pytest.mark.parametrize("n,S,C,dtype,with_vt", [
+    (2, 1024, 128, torch.bfloat16, True),   # C3 level 0: flash kernel
+    (1, 4096, 256, torch.bfloat16, True),   # Arch A at 256 px, level 2: flash kernel
+    (3, 320, 64, torch.bfloat16, True),     # flash kernel, ragged last key tile
+    (2, 64, 384, torch.bfloat16, True),     # Arch A level 2: whole-row MFMA kernel
+    (2, 16, 1024, torch.bfloat16, True),    # C3 level 3
+    (2, 4, 512, torch.bfloat16, False),     # C3 level 4: VALU kernel
+    (2, 1024, 128, torch.float32, False),   # parity mode
+    (3, 1, 256, torch.float32, False),      # C3 level 5 (S = 1: softmax of one key)
+])
+def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt):
+    gen = torch.Generator().manual_seed(S + C)
+    qkv = (torch.randn(n, S, 3 * C, generator=gen) * 1.5).to(dtype)
+    ref = _attn_ref(qkv)
+    d = qkv.cuda()
+    vt = d[:, :, 2 * C:].transpose(1, 2).contiguous() if with_vt else None
+    out = rt.attention(d, vt).float().cpu()
+    if dtype == torch.float32:
+        np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=5e-5, rtol=0)  # fp32, S-term sums
+    else:  # P and the output are rounded to bf16
+        assert _rel_l2(out, ref) < 1e-2
+        assert (out - ref).abs().max().item() < 3e-2 * ref.abs().max().item()

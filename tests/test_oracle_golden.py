@@ -8,7 +8,9 @@ import torch
 
 from conftest import golden
 from oracle import ref_cpu as R
-from itsd.arch import ARCH_A, ARCH_TINY, ARCH_TINY_CFG
+import dataclasses
+
+from itsd.arch import ARCH_A, ARCH_C, ARCH_TINY, ARCH_TINY_CFG
 from itsd.weights import synthetic_state_dict
 from itsd.schedule import make_schedule
 
@@ -55,6 +57,25 @@ def test_archA_eps():
     sd = synthetic_state_dict(ARCH_A, 0)
     with torch.no_grad():
         eps = _fw(ARCH_A, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]))
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def test_archC_eps():
+    """C3's CFG UNet at full size (547 M params; attention at S = 1024 ... 1)."""
+    g = golden("archC_eps")
+    sd = synthetic_state_dict(ARCH_C, 0)
+    with torch.no_grad():
+        eps = _fw(ARCH_C, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]), torch.from_numpy(g["labels"]))
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def test_archA64_eps():
+    """C4's Arch A at img_size 64."""
+    g = golden("archA64_eps")
+    a = dataclasses.replace(ARCH_A, img_size=64)
+    sd = synthetic_state_dict(a, 0)
+    with torch.no_grad():
+        eps = _fw(a, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]))
     np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
 
 

@@ -7,6 +7,7 @@ expected outputs only) to ``tests/golden/``. The reference's sampler prints
 every step; stdout is silenced while it runs.
 
     python tools/gen_golden.py            # regenerate everything
+    python tools/gen_golden.py archC_eps  # only the named fixture(s) of the "extra" group
 
 The GPU box never runs this (it has no /root/reference).
 """
@@ -29,7 +30,9 @@ OUT = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)
 
 import itsd  # noqa: E402
-from itsd.arch import ARCH_A, ARCH_TINY, ARCH_TINY_CFG  # noqa: E402
+import dataclasses  # noqa: E402
+
+from itsd.arch import ARCH_A, ARCH_C, ARCH_TINY, ARCH_TINY_CFG  # noqa: E402
 from itsd.weights import synthetic_state_dict  # noqa: E402
 
 
@@ -83,14 +86,45 @@ def noise_sequence(seed, shape, T):
     return xT, torch.stack(zs) if zs else torch.zeros((0,) + tuple(shape))
 
 
+def extra(M, MC, only):
+    """Full-size fixtures of the configs beyond C2 (outputs only; weights = recipe seed 0)."""
+    with torch.no_grad():
+        if not only or "archC_eps" in only:
+            # C3: the CFG UNet (MainCondition.py:10-13) at 32 px; attention at S = 1024 .. 1
+            a = ARCH_C
+            sd = synthetic_state_dict(a, seed=0)
+            net = ref_cfg(MC, a, sd)
+            g = torch.Generator().manual_seed(21)
+            x = torch.randn(2, 3, 32, 32, generator=g)
+            t = torch.tensor([10, 900])
+            lab = torch.tensor([4, 0])
+            save("archC_eps", x=x, t=t, labels=lab, eps=net(x, t, lab))
+            del net, sd
+        if not only or "archA64_eps" in only:
+            # C4: Arch A with img_size 64 (attention at S = 256)
+            a = dataclasses.replace(ARCH_A, img_size=64)
+            sd = synthetic_state_dict(a, seed=0)
+            net = ref_ddpm(M, a, sd)
+            g = torch.Generator().manual_seed(22)
+            x = torch.randn(2, 3, 64, 64, generator=g)
+            t = torch.tensor([3, 700])
+            save("archA64_eps", x=x, t=t, eps=net(x, t))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[1:]
     torch.set_num_threads(8)
     M = _load("ref_model", "Diffusion/Model.py")
     D = _load("ref_diffusion", "Diffusion/Diffusion.py")
     MC = _load("ref_model_cond", "DiffusionFreeGuidence/ModelCondition.py")
     DC = _load("ref_diffusion_cond", "DiffusionFreeGuidence/DiffusionCondition.py")
     S = _load("ref_search", "search/search_algorithm.py")
+    if only:
+        torch.set_num_threads(8)
+        extra(M, MC, only)
+        print("torch", torch.__version__)
+        return
     _stub_torchvision()
     with contextlib.redirect_stdout(io.StringIO()):
         V = _load("ref_verifier", "search/verifier.py")
@@ -215,6 +249,7 @@ def main():
         res.update(path_init=init, path_best_noise=bn, path_best_score=np.float64(bs),
                    path_scores=np.array(h["scores"]), path_nfes=ps.nfes)
         save("search_T5", **res)
+    extra(M, MC, None)
     print("torch", torch.__version__)
 
 
