@@ -36,6 +36,10 @@ hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
 bool conv_gn_eligible(int H, int W);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
+hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
+hipError_t launch_tail_mfma(const TailArgs&, hipStream_t);
+bool tail_mfma_ok(int H, int W, int C);
+int g_io_mfma = 1;  // bf16 head / tail on MFMA (itsd_set_option "io_mfma", read at create)
 hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
                         hipStream_t);
 }  // namespace itsd
@@ -137,6 +141,7 @@ struct itsd_unet {
 
   // fp32 params (arena offsets)
   size_t head_w = 0, head_b = 0, tail_w = 0, tail_b = 0;
+  size_t head_wmf = SIZE_MAX, tail_wmf = SIZE_MAX, tail_coef = SIZE_MAX;  // bf16 MFMA head / tail (+ tail GN coefficients)
   size_t freq = 0, ttable = 0, W0t = 0, b0 = 0, W2t = 0, b2 = 0, Wpt = 0, bp = 0;
   size_t ctable = 0, C1t = 0, cb1 = 0, C3t = 0, cb3 = 0, Wct = 0, bc = 0;
 
@@ -194,6 +199,11 @@ struct Builder {
     }
     ++used;
     return it->second.first;
+  }
+  // a second view of an entry already consumed by get/f32 (not counted again)
+  const float* peek(const std::string& name, int64_t numel) {
+    auto it = w.find(name);
+    return (it == w.end() || it->second.second != numel) ? nullptr : it->second.first;
   }
   size_t f32(const std::string& name, int64_t numel) {
     const float* p = get(name, numel);
@@ -425,6 +435,17 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   u->head_w = b.f32("head.weight", (int64_t)ch * 27);
   u->head_b = b.f32("head.bias", ch);
   u->head_out = b.act(H, H, ch);
+  if (u->bf16 && itsd::g_io_mfma && ch % 8 == 0 && ((H * H) % 128 == 0 || 128 % (H * H) == 0) &&
+      (H * H < 128 || 128 % H == 0)) {
+    // [Cout][32] bf16, k = ci*9 + tap (the reference's flat per-cout order), zero-padded
+    const float* hw = b.peek("head.weight", (int64_t)ch * 27);
+    if (hw) {
+      std::vector<uint16_t> wm((size_t)ch * 32, 0);
+      for (int co = 0; co < ch; ++co)
+        for (int k = 0; k < 27; ++k) wm[(size_t)co * 32 + k] = host_f2bf(hw[(size_t)co * 27 + k]);
+      u->head_wmf = b.ar.add(wm.data(), wm.size() * 2);
+    }
+  }
 
   std::vector<int> hs{u->head_out};
   int cur = u->head_out;
@@ -486,9 +507,29 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   u->tail_in = cur;
   u->tail_gn_g = b.f32("tail.0.weight", now);
   u->tail_gn_b = b.f32("tail.0.bias", now);
-  u->tail_g = b.act(H, H, now);
   u->tail_w = b.f32("tail.2.weight", (int64_t)3 * now * 9);
   u->tail_b = b.f32("tail.2.bias", 3);
+  if (u->bf16 && itsd::g_io_mfma && tail_mfma_ok(H, H, now)) {
+    // GroupNorm+SiLU fused into the MFMA tail: coefficients instead of a normalised copy;
+    // weights as [9C/32 k-steps][4 lane groups][3 couts][8 k] bf16, k = tap*C + ci
+    const float* tw = b.peek("tail.2.weight", (int64_t)3 * now * 9);
+    if (tw) {
+      const int nks = 9 * now / 32;
+      std::vector<uint16_t> wm((size_t)nks * 4 * 3 * 8);
+      for (int ks = 0; ks < nks; ++ks)
+        for (int kg = 0; kg < 4; ++kg)
+          for (int co = 0; co < 3; ++co)
+            for (int j = 0; j < 8; ++j) {
+              const int k = 32 * ks + 8 * kg + j, tap = k / now, ci = k - tap * now;
+              wm[(((size_t)ks * 4 + kg) * 3 + co) * 8 + j] = host_f2bf(tw[((size_t)co * now + ci) * 9 + tap]);
+            }
+      u->tail_wmf = b.ar.add(wm.data(), wm.size() * 2);
+    }
+    u->tail_coef = b.ws_off;
+    b.ws_off = (b.ws_off + (size_t)u->nb_max * now * 2 * 4 + 255) & ~(size_t)255;
+  } else {
+    u->tail_g = b.act(H, H, now);
+  }
 
   // all ResBlock temb_proj (and cond_proj) Linears as one [tdim][sumC] matrix
   {
@@ -706,25 +747,45 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     h.H = u->H; h.W = u->H; h.Cout = u->ch; h.n = c.nb; h.x_img_mod = c.x_mod;
     const Act& ho = u->acts[u->head_out];
     h.stats = ho.stats != SIZE_MAX ? (float*)(u->ws + ho.stats) : nullptr;
-    hipError_t e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
+    hipError_t e;
+    if (u->head_wmf != SIZE_MAX) {
+      h.wmf = (const bf16_t*)(u->wdev + u->head_wmf);
+      e = launch_head_mfma(h, s);
+    } else {
+      e = u->bf16 ? launch_head<bf16_t>(h, s) : launch_head<float>(h, s);
+    }
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   // census kinds: OpKind, and kCensusConvGN for the fused GroupNorm+SiLU convs
   for (const Op& o : u->ops)
     CHK(mark(o.kind == OP_CONV && o.coef != SIZE_MAX ? kCensusConvGN : (int)o.kind, op_flops(u, o, c.nb),
              [&]() { return launch_op(u, o, c, s); }));
-  // tail GN + conv (+ sampler update)
+  // tail GN + conv (+ sampler update); bf16 MFMA tail: GN coefficients, then one fused launch
   Op g;
-  g.kind = OP_GN;
-  g.src1 = u->tail_in; g.dst = u->tail_g; g.gamma = u->tail_gn_g; g.beta = u->tail_gn_b; g.silu = 1;
-  CHK(mark(OP_GN, 0.0, [&]() { return launch_op(u, g, c, s); }));
+  g.src1 = u->tail_in; g.gamma = u->tail_gn_g; g.beta = u->tail_gn_b; g.silu = 1;
+  if (u->tail_wmf != SIZE_MAX) {
+    g.kind = OP_GNCOEF;
+    g.coef = u->tail_coef;
+  } else {
+    g.kind = OP_GN;
+    g.dst = u->tail_g;
+  }
+  CHK(mark((int)g.kind, 0.0, [&]() { return launch_op(u, g, c, s); }));
   CHK(mark(-2, 2.0 * c.tail.n * (c.tail.cfg ? 2 : 1) * u->H * u->H * 27.0 * u->acts[u->tail_in].C, [&]() -> int {
     TailArgs t = c.tail;
-    t.g = u->ap(u->tail_g);
     t.w = u->wp(u->tail_w);
     t.b = u->wp(u->tail_b);
     t.H = u->H; t.W = u->H; t.C = u->acts[u->tail_in].C;
-    hipError_t e = u->bf16 ? launch_tail<bf16_t>(t, s) : launch_tail<float>(t, s);
+    hipError_t e;
+    if (u->tail_wmf != SIZE_MAX) {
+      t.g = u->ap(u->tail_in);
+      t.coef = (const float*)(u->ws + u->tail_coef);
+      t.wmf = (const bf16_t*)(u->wdev + u->tail_wmf);
+      e = launch_tail_mfma(t, s);
+    } else {
+      t.g = u->ap(u->tail_g);
+      e = u->bf16 ? launch_tail<bf16_t>(t, s) : launch_tail<float>(t, s);
+    }
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   return ITSD_OK;
@@ -794,6 +855,15 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "splitk")) {
     if (value < 0 || value > 64) return fail(ITSD_ERR_INVALID, "splitk in [0,64]");
     itsd::g_splitk = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "io_mfma")) {  // takes effect for UNets created afterwards
+    itsd::g_io_mfma = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "small_conv")) {
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "small_conv in [0,2]");
+    itsd::g_small_conv = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "conv_dbg")) {  // measurements only (results are wrong when set): 1 no

@@ -7,6 +7,7 @@
 namespace itsd {
 
 extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_set_option)
+extern int g_small_conv;   // 64x64-tile conv_small for small levels (itsd_set_option "small_conv")
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
@@ -125,6 +126,7 @@ struct HeadArgs {
   int H, W, Cout, n;
   int x_img_mod;        // image i reads x[i % x_img_mod] (CFG cond||uncond batch)
   float* stats;         // GroupNorm statistics slab of the output [slot][2][Cout], or null
+  const bf16_t* wmf;    // bf16 MFMA weights [Cout][32] (k = ci*9 + tap, zero-padded 27..31), or null
 };
 
 struct TailArgs {
@@ -146,6 +148,12 @@ struct TailArgs {
   long long noise_offset;  // Philox element offset (global candidate index * per-candidate elements)
   int clip_at;          // clip when t == clip_at (-1: never)
   int* nan_flag;
+  // bf16 MFMA tail (tail_mfma_kernel): g is the RAW last ResBlock output and the tail
+  // GroupNorm+SiLU is applied while staging it, with per-image coefficients
+  // coef[img][C/8][a0..a7, b0..b7] (gn_coef_kernel); wmf = bf16 weights [9C/32][4][3][8]
+  // (k = tap*C + ci; k-step ks, lane group kg, output channel, 8 consecutive k)
+  const float* coef;
+  const bf16_t* wmf;
 };
 
 }  // namespace itsd

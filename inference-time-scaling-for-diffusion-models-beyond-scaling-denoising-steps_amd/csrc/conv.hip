@@ -40,6 +40,7 @@ constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYT
 int g_fuse_gn = 1;
 int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
+int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -51,18 +52,27 @@ template <typename T>
 __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (&acc)[2][2], int wm, int wn, int rl,
                                           int hh) {
   if constexpr (sizeof(T) == 2) {
+    // fragment reads two k-steps ahead of their MFMAs (<= 12 LDS reads outstanding: the
+    // 4-bit lgkmcnt then counts them, and each k-step waits only for its own 4 reads)
+    bf16x8 af[4][2], bfg[4][2];
+    auto rd = [&](int kk) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[kk][i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfg[kk][j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
+    };
+    rd(0);
+    rd(1);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 af[2], bfg[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfg[j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
+      if (kk + 2 < 4) rd(kk + 2);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfg[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   } else {
     // k mapping for the f32 MFMA: step s, lane half h -> k = 16h + s (A and B alike).
@@ -93,7 +103,7 @@ __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (
 // 3. per-channel (sum, sum of squares) over each pixel slot of the tile: the
 //    GroupNorm statistics of the consumer (Model.py:171,180), written as a
 //    deterministic partial slab stats[slot][2][Cout] (no atomics).
-template <typename T>
+template <typename T, int BM = 128, int BN = 128>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
 
 // accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
@@ -121,9 +131,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
 
 // E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
 // and the consumer GroupNorm's statistics slab.
-template <typename T>
+template <typename T, int BM, int BN>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
   constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int ER = BM + 4;  // E row (floats): 128x128 tile -> EROW
   const int NT = blockDim.x;
   const int tid = threadIdx.x;
   const int HWo = a.Hout * a.Wout;
@@ -138,8 +149,8 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
     // channel-major store of this (whole-V) tile: vt[img][c][pixel], 16-B chunks of
     // consecutive pixels of one image (host: HWo % EPC == 0, vt_from % 128 == 0); + bias only.
     const int Cv = a.Cout - a.vt_from;
-    for (int it = tid; it < 128 * (128 / EPC); it += NT) {
-      const int cl = it / (128 / EPC), pl = (it - cl * (128 / EPC)) * EPC;
+    for (int it = tid; it < BM * (BN / EPC); it += NT) {
+      const int cl = it / (BN / EPC), pl = (it - cl * (BN / EPC)) * EPC;
       const int co = tileC + cl, p = tileP + pl;
       if (co >= a.Cout || p >= a.M) continue;
       const int img = p / HWo, pi = p - img * HWo;
@@ -147,7 +158,7 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
       u32x4 w;
       T* we = (T*)&w;
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(E[(pl + e) * EROW + cl] + bb);
+      for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(E[(pl + e) * ER + cl] + bb);
       *(u32x4*)((T*)a.vt_out + ((size_t)img * Cv + (co - a.vt_from)) * HWo + pi) = w;
     }
     return;
@@ -155,13 +166,13 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
   // Additive vectors bias + temb row + CFG cond row per (image of the tile, cout),
   // staged once in LDS (the statistics scratch R, free until the statistics pass).
   // Host: the tile's pixels span whole images (HWo % 128 == 0) or 128 % HWo == 0.
-  float* addv = E + 128 * EROW;  // [<= 8 images][128]
+  float* addv = E + BN * ER;  // [images of the tile][BM]
   const int img0 = tileP / HWo;
-  const int nimt = HWo >= 128 ? 1 : 128 / HWo;
+  const int nimt = HWo >= BN ? 1 : BN / HWo;
   {
     const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tid; it < nimt * 128; it += NT) {
-      const int il = it >> 7, cl = it & 127, co = tileC + cl, img = img0 + il;
+    for (int it = tid; it < nimt * BM; it += NT) {
+      const int il = it / BM, cl = it % BM, co = tileC + cl, img = img0 + il;
       float v = 0.f;
       if (co < a.Cout && (long long)img * HWo < a.M) {
         v = a.bias[co];
@@ -175,10 +186,10 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
       addv[it] = v;
     }
   }
-  constexpr int CPR = 128 / EPC;  // 16-B output chunks per tile row
+  constexpr int CPR = BM / EPC;  // 16-B output chunks per tile row
   const int cl = (tid % CPR) * EPC, co = tileC + cl;
   const int RPI = NT / CPR;       // rows per pass
-  constexpr int MAXR = 128 * CPR / 256;
+  constexpr int MAXR = (BN * CPR + 255) / 256;
   // residual rows first: all loads in flight before the first use
   u32x4 rres[MAXR];
   if (a.resid) {
@@ -186,7 +197,7 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
     for (int k = 0; k < MAXR; ++k) {
       const int pl = tid / CPR + k * RPI;
       const int p = tileP + pl;
-      rres[k] = (pl < 128 && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + orow(p) * a.Cout + co)
+      rres[k] = (pl < BN && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + orow(p) * a.Cout + co)
                                                       : u32x4{0u, 0u, 0u, 0u};
     }
   }
@@ -195,12 +206,12 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
   for (int k = 0; k < MAXR; ++k) {
     const int pl = tid / CPR + k * RPI;
     const int p = tileP + pl;
-    if (pl >= 128 || p >= a.M || co >= a.Cout) continue;
-    const float* av = addv + ((HWo >= 128 ? 0 : pl / HWo) << 7) + cl;
+    if (pl >= BN || p >= a.M || co >= a.Cout) continue;
+    const float* av = addv + (HWo >= BN ? 0 : pl / HWo) * BM + cl;
     float v[EPC];
 #pragma unroll
     for (int q = 0; q < EPC / 4; ++q) {
-      const f32x4 e4 = *(const f32x4*)(E + pl * EROW + cl + 4 * q);
+      const f32x4 e4 = *(const f32x4*)(E + pl * ER + cl + 4 * q);
       const f32x4 b4 = *(const f32x4*)(av + 4 * q);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
@@ -221,55 +232,55 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
         f32x4 s4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) s4[e] = Elem<T>::tof(we[4 * q + e]);
-        *(f32x4*)(E + pl * EROW + cl + 4 * q) = s4;
+        *(f32x4*)(E + pl * ER + cl + 4 * q) = s4;
       }
     }
   }
   if (a.stats) {
     __syncthreads();
     const int Gt = stat_slot_px(HWo);  // host guarantees 128 % HWo == 0 or HWo % 128 == 0
-    const int S = 128 / Gt;
+    const int S = BN / Gt;
     if (Gt >= 16) {
-      // pass 1: 8 groups of 16 pixel rows x 32 channel quads, 16-B LDS reads
-      float* R = E + 128 * EROW;  // [8 groups][2][128]
-      if (tid < 256) {
-        const int cq = tid & 31, pg = tid >> 5;
+      // pass 1: BN/16 groups of 16 pixel rows x BM/4 channel quads, 16-B LDS reads
+      float* R = E + BN * ER;  // [BN/16 groups][2][BM]
+      if (tid < (BN / 16) * (BM / 4)) {
+        const int cq = tid % (BM / 4), pg = tid / (BM / 4);
         f32x4 s4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
         for (int k = 0; k < 16; ++k) {
           const int pl = pg * 16 + k;
           if (tileP + pl < a.M) {
-            const f32x4 v = *(const f32x4*)(E + pl * EROW + 4 * cq);
+            const f32x4 v = *(const f32x4*)(E + pl * ER + 4 * cq);
             s4 += v;
             q4 += v * v;
           }
         }
-        *(f32x4*)(R + (pg * 2) * 128 + 4 * cq) = s4;
-        *(f32x4*)(R + (pg * 2 + 1) * 128 + 4 * cq) = q4;
+        *(f32x4*)(R + (pg * 2) * BM + 4 * cq) = s4;
+        *(f32x4*)(R + (pg * 2 + 1) * BM + 4 * cq) = q4;
       }
       __syncthreads();
       // pass 2: groups -> slots in fixed order (deterministic)
       const int gps = Gt / 16;
-      for (int item = tid; item < S * 128; item += NT) {
-        const int s = item >> 7, cl = item & 127;
+      for (int item = tid; item < S * BM; item += NT) {
+        const int s = item / BM, cl = item % BM;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
         float sum = 0.f, sq = 0.f;
         for (int g = s * gps; g < (s + 1) * gps; ++g) {
-          sum += R[(g * 2) * 128 + cl];
-          sq += R[(g * 2 + 1) * 128 + cl];
+          sum += R[(g * 2) * BM + cl];
+          sq += R[(g * 2 + 1) * BM + cl];
         }
         const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * (HWo / 128) + phase * (HWo / 128) + (p0 % HWo) / 128;
         a.stats[(slot * 2) * a.Cout + co] = sum;
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
     } else {
-      for (int item = tid; item < S * 128; item += NT) {
-        const int s = item >> 7, cl = item & 127;
+      for (int item = tid; item < S * BM; item += NT) {
+        const int s = item / BM, cl = item % BM;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
         float sum = 0.f, sq = 0.f;
         for (int k = 0; k < Gt; ++k) {
-          const float v = E[(s * Gt + k) * EROW + cl];
+          const float v = E[(s * Gt + k) * ER + cl];
           sum += v;
           sq = fmaf(v, v, sq);
         }
@@ -486,6 +497,122 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   }
   if (a.dbg & 16) return;
   conv_epilogue<T>(a, acc, smem, tileP, tileC, phase);
+}
+
+// ---------------------------------------------------------------------------- small tiles
+// The 8x8 / 4x4 / 2x2 / 1x1 levels (M = n * HWo <= 64 n): 128 x 128 tiles leave most of
+// the 256 CUs idle (4x4 level, n = 256: 128 tiles), and split-K buys the parallelism
+// back with an fp32 partial round trip and a second launch. A 64 couts x 64 pixels tile
+// gives 4x the blocks with the whole K in one block: 4 waves in 2x2, each one 32x32
+// v_mfma_f32_32x32x16_bf16 accumulator; LDS images [64 rows][128 B] (same swizzle), a
+// 4-deep global_load_lds ring (16 KB per stage, 3 stages in flight), 2 blocks per CU.
+// The epilogue is the shared one at 64 x 64 (host: 64 % HWo == 0, so a tile holds whole
+// images and whole GroupNorm statistics slots).
+constexpr int SM_B = 64;                    // couts and pixels per small tile
+constexpr int SM_TILEB = SM_B * ROWB;       // 8 KB
+constexpr int SM_NS = 4;
+constexpr int SM_EPI = SM_B * (SM_B + 4) * 4 + SM_B * SM_B * 4;  // E + (addv | statistics groups)
+constexpr int SM_SMEM = (SM_NS * 2 * SM_TILEB > SM_EPI) ? SM_NS * 2 * SM_TILEB : SM_EPI;
+
+__global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int BK = 64, STAGE = 2 * SM_TILEB;
+  __shared__ __attribute__((aligned(16))) char smem[SM_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, rl = lane & 31, hh = lane >> 5;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * SM_B, tileC = bt.y * SM_B;
+  const int Cin = a.C1 + a.C2, cpt = Cin / BK, nK = a.ksize * a.ksize * cpt;
+  const int HWo = a.Hout * a.Wout;
+  const T* zero = zero_of_block<T>(a);
+  // DMA rows: instruction q of wave w fills rows 8*(2w+q) .. +7 of the A and B images
+  const T* arow[2];
+  int pix1[2], pix2[2];
+  unsigned tmask[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * (2 * wid + q) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int co = tileC + r;
+    arow[q] = co < a.Cout ? (const T*)a.wt + (size_t)co * a.K + c * 8 : nullptr;
+    const int p = tileP + r;
+    const bool pv = p < a.M;
+    const int img = p / HWo, rem = p - img * HWo, oy = rem / a.Wout;
+    const int iy0 = oy * a.stride - a.pad, ix0 = (rem - oy * a.Wout) * a.stride - a.pad;
+    const int pl = (img * a.Hin + iy0) * a.Win + ix0;
+    pix1[q] = pl * a.C1 + c * 8;
+    pix2[q] = pl * a.C2 + c * 8;
+    unsigned m = 0;
+    for (int ky = 0; ky < a.ksize; ++ky)
+      for (int kx = 0; kx < a.ksize; ++kx) {
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        if (pv && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win) m |= 1u << (ky * a.ksize + kx);
+      }
+    tmask[q] = m;
+  }
+  auto issue = [&](int kc) {
+    const int tap = kc / cpt, ci0 = (kc - tap * cpt) * BK;
+    const int ky = tap / a.ksize, kx = tap - ky * a.ksize;
+    char* sA = smem + (kc % SM_NS) * STAGE;
+    char* sB = sA + SM_TILEB;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int toff = (ky * a.Win + kx) * (s1 ? a.C1 : a.C2) + (s1 ? ci0 : ci0 - a.C1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const T* ga = arow[q] ? arow[q] + (size_t)kc * BK : zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sA + (2 * wid + q) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const T* gb = ((tmask[q] >> tap) & 1u) ? src + (s1 ? pix1[q] : pix2[q]) + toff : zero;
+      __builtin_amdgcn_global_load_lds((const void*)gb, (lds_ptr_t)(sB + (2 * wid + q) * 1024), 16, 0, 0);
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < SM_NS - 1; ++s)
+    if (s < nK) issue(s);
+  for (int kc = 0; kc < nK; ++kc) {
+    const int ahead = min(SM_NS - 2, nK - 1 - kc);  // younger stages kept in flight (4 DMA each)
+    if (ahead >= 2) wait_vmcnt<8>();
+    else if (ahead == 1) wait_vmcnt<4>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kc + SM_NS - 1 < nK) issue(kc + SM_NS - 1);
+    const char* A = smem + (kc % SM_NS) * STAGE;
+    const char* B = A + SM_TILEB;
+    bf16x8 af[4], bf[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      af[kk] = *(const bf16x8*)(A + swz(wm * 32 + rl, 2 * kk + hh));
+      bf[kk] = *(const bf16x8*)(B + swz(wn * 32 + rl, 2 * kk + hh));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], bf[kk], acc, 0, 0, 0);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // accumulators -> E[pixel][cout] (row SM_B + 4 floats)
+  float* E = (float*)smem;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    f32x4 v4 = {acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+    *(f32x4*)(E + (wn * 32 + rl) * (SM_B + 4) + wm * 32 + 8 * g + 4 * hh) = v4;
+  }
+  __syncthreads();
+  epilogue_from_E<T, SM_B, SM_B>(a, smem, tileP, tileC, -1);
+}
+
+// Host-side eligibility of conv_small (bf16, whole 128-B K-chunks, plain stride/pad addressing).
+bool conv_small_ok(const ConvArgs& a) {
+  const int HWo = a.Hout * a.Wout, Cin = a.C1 + a.C2;
+  return a.zero && !a.subpix && !a.upsample && !a.zins && !a.gn_coef && Cin % 64 == 0 && a.C1 % 64 == 0 &&
+         a.K == a.ksize * a.ksize * Cin && a.ksize <= 5 && HWo <= SM_B && SM_B % HWo == 0 &&
+         (!a.vt_out || HWo % 8 == 0);
 }
 
 template <typename T>
@@ -772,21 +899,29 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
     if (a.dbg & 2) return;
     const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
     const char* A = wring + (s % GNC_NS) * TILEB;
+    // fragment reads two k-steps ahead of their MFMAs (see mma_stage)
+    bf16x8 af[4][2], bfg[4][2];
+    auto rd = [&](int kk) {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 af[2], bfg[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+      for (int i = 0; i < 2; ++i) af[kk][i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int h = hb[j] + toff;
-        bfg[j] = *(const bf16x8*)(halo + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
+        bfg[kk][j] = *(const bf16x8*)(halo + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
       }
+    };
+    rd(0);
+    rd(1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk + 2 < 4) rd(kk + 2);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfg[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -893,6 +1028,101 @@ hipError_t launch_gn_coef(const GNArgs& g, int n, float* coef, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- head on MFMA
+// head = Conv2d(3, ch, 3, padding=1) (Model.py:219, ModelCondition.py:170) in bf16 mode as
+// an MFMA GEMM with K = 27 zero-padded to 32: D[cout][pixel] = W[cout][k] x patch[k][pixel],
+// k = ci*9 + ky*3 + kx. Block = 128 pixels (whole image rows, one GroupNorm statistics slot
+// or whole images) x 128 couts; the 3-channel input window sits in LDS as fp32, each lane
+// builds its pixel's two 8-element k-fragments from it; the shared epilogue adds the bias,
+// rounds, stores NHWC and writes the first GroupNorm's statistics slab.
+__global__ __launch_bounds__(256, 2) void head_mfma_kernel(HeadArgs h) {
+  __shared__ __attribute__((aligned(16))) char smem[EPI_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int HW = h.H * h.W, W = h.W;
+  const long long tileP = (long long)blockIdx.x * 128;
+  const int tileC = blockIdx.y * 128;
+  // input window: rows covering the tile's 128 pixels (+1 border), all images of the tile
+  const int img0 = (int)(tileP / HW), r0 = (int)(tileP - (long long)img0 * HW);
+  const int nimg = HW >= 128 ? 1 : 128 / HW;          // images per tile
+  const int rows = HW >= 128 ? 128 / W : h.H;         // output rows per image in the tile
+  const int y0 = r0 / W, TR = rows + 2, TW = W + 2;
+  float* tin = (float*)smem + 128 * 132;              // [nimg][3][TR][TW] behind the epilogue's E tile
+  for (int i = tid; i < nimg * 3 * TR * TW; i += 256) {
+    const int im = i / (3 * TR * TW), r = i - im * 3 * TR * TW;
+    const int ci = r / (TR * TW), q = r - ci * TR * TW, ty = q / TW, tx = q - ty * TW;
+    const int iy = y0 - 1 + ty, ix = tx - 1, img = img0 + im;
+    float v = 0.0f;
+    if (img < h.n && iy >= 0 && iy < h.H && ix >= 0 && ix < W)
+      v = h.x[((size_t)(img % h.x_img_mod) * 3 + ci) * HW + iy * W + ix];
+    tin[i] = v;
+  }
+  // A fragments (weights) straight from the prepacked [Cout][32] bf16 matrix
+  bf16x8 af[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = tileC + mb * 32 + rl;
+      af[mb][s] = co < h.Cout ? *(const bf16x8*)(h.wmf + (size_t)co * 32 + 16 * s + 8 * hh)
+                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  __syncthreads();
+  // B fragment of this lane's pixel (column rl of wave wid's 32 pixels)
+  const int pl = wid * 32 + rl;
+  const int im = HW >= 128 ? 0 : pl / HW, pr = HW >= 128 ? pl : pl - im * HW;
+  const int ly = pr / W, lx = pr - ly * W;
+  bf16x8 bfr[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * hh + j;
+      float v = 0.0f;
+      if (k < 27) {
+        const int ci = k / 9, tap = k - ci * 9, ky = tap / 3, kx = tap - ky * 3;
+        v = tin[((im * 3 + ci) * TR + ly + ky) * TW + lx + kx];
+      }
+      bfr[s][j] = (short)f2bf(v);
+    }
+  f32x16 acc[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[mb][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) acc[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb][s], bfr[s], acc[mb], 0, 0, 0);
+  }
+  __syncthreads();  // tin is dead; E[pixel][cout] overlays the front of smem
+  float* E = (float*)smem;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v4 = {acc[mb][4 * g], acc[mb][4 * g + 1], acc[mb][4 * g + 2], acc[mb][4 * g + 3]};
+      *(f32x4*)(E + pl * EROW + mb * 32 + 8 * g + 4 * hh) = v4;
+    }
+  __syncthreads();
+  ConvArgs a{};
+  a.bias = h.b;
+  a.out = h.out;
+  a.Cout = h.Cout;
+  a.Hout = h.H; a.Wout = h.W;
+  a.M = h.n * HW;
+  a.stats = h.stats;
+  epilogue_from_E<bf16_t>(a, smem, (int)tileP, tileC, -1);
+}
+
+hipError_t launch_head_mfma(const HeadArgs& h, hipStream_t s) {
+  const int HW = h.H * h.W;
+  const int nimg = HW >= 128 ? 1 : 128 / HW, rows = HW >= 128 ? 128 / h.W : h.H;
+  if (!h.wmf || (HW % 128 && 128 % HW) || (HW >= 128 && 128 % h.W) || h.Cout % 8 ||
+      (size_t)(128 * 132 + nimg * 3 * (rows + 2) * (h.W + 2)) * 4 > (size_t)EPI_BYTES)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_mfma_kernel, dim3((unsigned)(((long long)h.n * HW + 127) / 128), (h.Cout + 127) / 128), dim3(256), 0,
+                     s, h);
+  return hipGetLastError();
+}
+
 // Host-side eligibility of the fused kernel at an HxW level (the builder decides per conv).
 bool conv_gn_eligible(int H, int W) {
   if (W > 128 || 128 % W) return false;
@@ -915,6 +1145,14 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   }
   constexpr int BK = 8 * (16 / (int)sizeof(T));
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+  if constexpr (sizeof(T) == 2) {
+    // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
+    // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
+    if (g_small_conv && conv_small_ok(a) && (g_small_conv == 2 || (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024))) {
+      hipLaunchKernelGGL(conv_small, dim3((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   const int Cin = a.C1 + a.C2;
   const bool pipe = a.zero && Cin % BK == 0 && a.C1 % BK == 0 && a.K == a.ksize * a.ksize * Cin;
   const int v = g_conv_variant;

@@ -62,21 +62,36 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
   const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
   const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
   T* dst = (T*)a.dst + (size_t)img * a.HW * C;
-  for (unsigned idx = c0 + tid; idx < c1; idx += 256) {
-    const int p = (int)(idx / cpp);
-    const int c = (int)(idx - (unsigned)p * cpp) * EPC;
-    const u32x4 x = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c)
-                             : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
-    const T* xe = (const T*)&x;
-    u32x4 y;
-    T* ye = (T*)&y;
+  // batches of 4 chunks per thread: all 4 loads in flight before the first use
+  for (unsigned i0 = c0; i0 < c1; i0 += 4 * 256) {
+    u32x4 x[4];
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) {
-      float v = Elem<T>::tof(xe[e]) * coef[0][c + e] + coef[1][c + e];
-      if (a.silu) v = silu(v);
-      ye[e] = Elem<T>::to(v);
+    for (int u = 0; u < 4; ++u) {
+      const unsigned idx = i0 + u * 256 + tid;
+      x[u] = u32x4{0u, 0u, 0u, 0u};
+      if (idx < c1) {
+        const int p = (int)(idx / cpp);
+        const int c = (int)(idx - (unsigned)p * cpp) * EPC;
+        x[u] = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c) : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
+      }
     }
-    *(u32x4*)(dst + (size_t)p * C + c) = y;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned idx = i0 + u * 256 + tid;
+      if (idx >= c1) continue;
+      const int p = (int)(idx / cpp);
+      const int c = (int)(idx - (unsigned)p * cpp) * EPC;
+      const T* xe = (const T*)&x[u];
+      u32x4 y;
+      T* ye = (T*)&y;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        float v = Elem<T>::tof(xe[e]) * coef[0][c + e] + coef[1][c + e];
+        if (a.silu) v = silu(v);
+        ye[e] = Elem<T>::to(v);
+      }
+      *(u32x4*)(dst + (size_t)p * C + c) = y;
+    }
   }
 }
 
@@ -701,6 +716,154 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
     if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
     a.x[o] = xn;
   }
+}
+
+// bf16 tail on MFMA with the tail GroupNorm+SiLU fused (Model.py:252-256 / 282, then the
+// sampler step as tail2_kernel). Block = 128 output pixels (128/W rows) of one image; the
+// raw input halo ((128/W + 2) x (W + 2) pixels x C) is staged once in LDS with
+// y = silu(x*a + b) applied (padding stays 0), at a padded pixel stride (conflict-free
+// 16-B fragment reads); the staging issues 8 loads per thread before transforming any
+// (HBM latency once per batch, not per chunk). Each wave owns 2 x 16 pixels:
+// eps[pixel][co] = sum_k patch[pixel][k] W[co][k] on v_mfma_f32_16x16x32_bf16
+// (k = tap*C + ci; 9C/32 k-steps; B columns 3..15 are zero).
+constexpr int TM_PX = 128;  // output pixels per block
+__global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int C = a.C, W = a.W, H = a.H, HW = H * W;
+  const int rpb = TM_PX / W, bpi = H / rpb, PST = 2 * C + 16, NKS = 9 * C / 32;
+  const int img = blockIdx.x / bpi, y0 = (blockIdx.x % bpi) * rpb;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  bf16x8* wl = (bf16x8*)tsm;                                   // [NKS][4][3]
+  char* halo = tsm + NKS * 12 * 16;                            // [(rpb+2)*(W+2)][PST]
+  float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);     // [2 passes][TM_PX][3]
+  for (int i = tid; i < NKS * 12; i += 256) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
+  const int m = lane & 15, kg = lane >> 4;
+  int hbase[2];
+#pragma unroll
+  for (int gi = 0; gi < 2; ++gi) {
+    const int pl = wid * 32 + gi * 16 + m, py = pl / W, px = pl - py * W;
+    hbase[gi] = (py * (W + 2) + px) * PST + 16 * kg;
+  }
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int cpp = C / 8, npx = (rpb + 2) * (W + 2), total = npx * cpp;
+  for (int pass = 0; pass < (a.cfg ? 2 : 1); ++pass) {
+    const int im = img + pass * a.n;
+    __syncthreads();
+    const bf16_t* gb = (const bf16_t*)a.g + (size_t)im * HW * C;
+    const float* cf = a.coef + (size_t)im * cpp * 16;
+    for (int i0 = 0; i0 < total; i0 += 8 * 256) {
+      u32x4 v[8];
+      int dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // all loads of the batch first
+        const int i = i0 + u * 256 + tid;
+        const int hp = i / cpp, ch = i - hp * cpp;
+        const int hy = hp / (W + 2), hx = hp - hy * (W + 2);
+        const int gy = y0 - 1 + hy, gx = hx - 1;
+        const bool ok = i < total && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        dst[u] = i < total ? hp * PST + ch * 16 : -1;
+        v[u] = ok ? *(const u32x4*)(gb + ((size_t)gy * W + gx) * C + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+        if (!ok) dst[u] = i < total ? -2 - dst[u] : -1;  // padding: store zeros at -2 - dst
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (dst[u] == -1) continue;
+        u32x4 y = {0u, 0u, 0u, 0u};
+        int d = dst[u];
+        if (d >= 0) {
+          const int ch = (d % PST) / 16;
+          const f32x4* cp = (const f32x4*)(cf + ch * 16);
+          const f32x4 a0 = cp[0], a1 = cp[1], b0 = cp[2], b1 = cp[3];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const float x0 = __uint_as_float(v[u][w] << 16), x1 = __uint_as_float(v[u][w] & 0xffff0000u);
+            const float s0 = w < 2 ? a0[2 * w] : a1[2 * w - 4], s1 = w < 2 ? a0[2 * w + 1] : a1[2 * w - 3];
+            const float t0 = w < 2 ? b0[2 * w] : b1[2 * w - 4], t1 = w < 2 ? b0[2 * w + 1] : b1[2 * w - 3];
+            y[w] = (uint32_t)f2bf(silu(x0 * s0 + t0)) | ((uint32_t)f2bf(silu(x1 * s1 + t1)) << 16);
+          }
+        } else {
+          d = -2 - d;
+        }
+        *(u32x4*)(halo + d) = y;
+      }
+    }
+    __syncthreads();
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int cpt = C / 32;
+#pragma unroll 4
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int tap = ks / cpt, ci0 = (ks - tap * cpt) * 32;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int toff = (ky * (W + 2) + kx) * PST + ci0 * 2;
+      const bf16x8 bw = m < 3 ? wl[(ks * 4 + kg) * 3 + m] : z8;
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        const bf16x8 af = *(const bf16x8*)(halo + hbase[gi] + toff);
+        acc[gi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[gi], 0, 0, 0);
+      }
+    }
+    // D[pixel 4*kg + i][co = m] of this wave's two 16-pixel groups
+    if (m < 3) {
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(pass * TM_PX + wid * 32 + gi * 16 + 4 * kg + i) * 3 + m] = acc[gi][i];
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < TM_PX * 3; it += 256) {
+    const int opx = it / 3, oc = it - opx * 3;
+    float e = red[opx * 3 + oc] + a.b[oc];
+    if (a.cfg) {
+#pragma clang fp contract(off)
+      const float u = red[(TM_PX + opx) * 3 + oc] + a.b[oc];
+      e = a.guide_w1 * e - a.guide_w * u;
+    }
+    const int rem = (y0 + opx / W) * W + (opx - (opx / W) * W);
+    const size_t o = ((size_t)img * 3 + oc) * HW + rem;
+    if (!a.step_mode) {
+      a.eps_out[o] = e;
+      continue;
+    }
+    {
+#pragma clang fp contract(off)
+      const int t = *a.tsel;
+      const float xv = a.x[o];
+      const float mean = a.coeff1[t] * xv - a.coeff2[t] * e;
+      float xn = mean;
+      if (t > 0) {
+        const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o]
+                                : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+        xn = mean + a.sqrt_var[t] * z;
+      }
+      if (xn != xn) atomicOr(a.nan_flag, 1);
+      if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+      a.x[o] = xn;
+    }
+  }
+}
+
+size_t tail_mfma_smem(int H, int W, int C) {
+  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(TM_PX / W + 2) * (W + 2) * (2 * C + 16) + 2 * TM_PX * 3 * 4;
+}
+
+bool tail_mfma_ok(int H, int W, int C) {
+  return W <= TM_PX && TM_PX % W == 0 && TM_PX / W <= H && H % (TM_PX / W) == 0 && C % 32 == 0 &&
+         tail_mfma_smem(H, W, C) <= 160 * 1024;
+}
+
+hipError_t launch_tail_mfma(const TailArgs& a, hipStream_t s) {
+  if (!a.coef || !a.wmf || !tail_mfma_ok(a.H, a.W, a.C)) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)tail_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(tail_mfma_kernel, dim3(a.n * (a.H / (TM_PX / a.W))), dim3(256), tail_mfma_smem(a.H, a.W, a.C), s,
+                     a);
+  return hipGetLastError();
 }
 
 template <typename T>

@@ -127,6 +127,18 @@ def test_trajectory_cfg_fp32_vs_reference():
     np.testing.assert_allclose(x0, g["x0"], atol=TRAJ_TOL_FP32, rtol=0)
 
 
+def test_trajectory_cfg_bf16_vs_reference():
+    """Guided bf16 sampler (cond || uncond batch through the MFMA tail with the fused
+    tail GroupNorm) against the reference trajectory: relative L2 <= 3e-2 after T = 6."""
+    g = golden("tiny_cfg_traj")
+    T = int(g["T"])
+    net = _net(ARCH_TINY_CFG, "bf16")
+    smp = CondGaussianDiffusionSampler(net, 1e-4, 0.028, T, w=float(g["w"]))
+    noise = torch.cat([torch.zeros(1, 2, 3, 32, 32), torch.from_numpy(g["noise"]).flip(0)])
+    x0 = smp(torch.from_numpy(g["x_T"]).cuda(), torch.from_numpy(g["labels"]).cuda(), noise=noise).cpu()
+    assert _rel_l2(x0, torch.from_numpy(g["x0"])) < 3e-2
+
+
 def test_trajectory_archA_fp32_vs_reference():
     g = golden("archA_traj")
     T = int(g["T"])

@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
     ap.add_argument("--fuse-gn", type=int, default=1, help="fused GroupNorm+SiLU+conv3x3 in ResBlocks")
+    ap.add_argument("--io-mfma", type=int, default=1, help="bf16 head/tail on MFMA (tail GroupNorm fused)")
     args = ap.parse_args()
     from itsd import runtime as rt
     rt.set_option("fuse_gn", args.fuse_gn)
+    rt.set_option("io_mfma", args.io_mfma)
     a = ARCH_A
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=args.precision, weights="gauss")
     net.to("cuda:0")
@@ -35,14 +37,18 @@ def main():
     x = torch.randn(args.n, 3, 32, 32, device="cuda")
     t = torch.full((args.n,), 500, dtype=torch.int32, device="cuda")
     if args.variants:
-        from itsd import runtime as rt
+        # each variant: '+'-joined itsd_set_option key=value pairs, e.g.
+        # "base", "small_conv=0", "conv_variant=2+splitk=0", "conv_dbg=19"
+        defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1}
         for rnd in range(3):
-            for v in args.variants.split(","):  # e.g. "2", "2s0" (split-K off), "2s1d1" (debug: no loads)
-                v0, _, dbg = v.partition("d")
-                vv, _, sk = v0.partition("s")
-                rt.set_option("conv_variant", int(vv))
-                rt.set_option("splitk", int(sk) if sk else 1)
-                rt.set_option("conv_dbg", int(dbg) if dbg else 0)
+            for v in args.variants.split(","):
+                opts = dict(defaults)
+                for kv in v.split("+"):
+                    if "=" in kv:
+                        k, val = kv.split("=")
+                        opts[k] = int(val)
+                for k, val in opts.items():
+                    rt.set_option(k, val)
                 ops = nat.profile_ops(x, t)
                 conv = [o for o in ops if o["kind"] in ("conv", "convgn")]
                 by = defaultdict(lambda: [0.0, 0.0])
@@ -51,9 +57,8 @@ def main():
                     by[o["H"]][1] += o["flops"]
                 print(f"round {rnd} variant {v}: conv {sum(o['ms'] for o in conv):.3f} ms total {sum(o['ms'] for o in ops):.3f} ms | "
                       + " ".join(f"H{h}:{m:.3f}ms/{f / m / 1e9:.0f}TF" for h, (m, f) in sorted(by.items())))
-        rt.set_option("conv_variant", 2)
-        rt.set_option("splitk", 1)
-        rt.set_option("conv_dbg", 0)
+        for k, val in defaults.items():
+            rt.set_option(k, val)
     for _ in range(args.reps):
         ops = nat.profile_ops(x, t)
     tot = sum(o["ms"] for o in ops)
