@@ -867,8 +867,11 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "conv_dbg")) {  // measurements only (results are wrong when set): 1 no
-    // in-loop loads, 2 no MFMA, 4 no GN statistics, 8 no GN transform, 16 no epilogue
-    itsd::g_conv_dbg = value & 31;
+    // in-loop loads (zero-page sources), 2 no MFMA, 8 no GN transform, 16 no epilogue,
+    // 32 no epilogue output stores, 64 fused-conv halo loads from the zero page, 128 no
+    // GN statistics pass, 256 no residual loads. (Never skip an issued load's wait: an
+    // in-flight load landing in a reused register faults.)
+    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256);
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards

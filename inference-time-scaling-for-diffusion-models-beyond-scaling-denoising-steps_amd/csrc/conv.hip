@@ -52,27 +52,18 @@ template <typename T>
 __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (&acc)[2][2], int wm, int wn, int rl,
                                           int hh) {
   if constexpr (sizeof(T) == 2) {
-    // fragment reads two k-steps ahead of their MFMAs (<= 12 LDS reads outstanding: the
-    // 4-bit lgkmcnt then counts them, and each k-step waits only for its own 4 reads)
-    bf16x8 af[4][2], bfg[4][2];
-    auto rd = [&](int kk) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[kk][i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfg[kk][j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
-    };
-    rd(0);
-    rd(1);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      if (kk + 2 < 4) rd(kk + 2);
-      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 af[2], bfg[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfg[j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfg[kk][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
   } else {
     // k mapping for the f32 MFMA: step s, lane half h -> k = 16h + s (A and B alike).
@@ -197,8 +188,9 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
     for (int k = 0; k < MAXR; ++k) {
       const int pl = tid / CPR + k * RPI;
       const int p = tileP + pl;
-      rres[k] = (pl < BN && p < a.M && co < a.Cout) ? *(const u32x4*)((const T*)a.resid + orow(p) * a.Cout + co)
-                                                      : u32x4{0u, 0u, 0u, 0u};
+      rres[k] = (pl < BN && p < a.M && co < a.Cout && !(a.dbg & 256))
+                    ? *(const u32x4*)((const T*)a.resid + orow(p) * a.Cout + co)
+                    : u32x4{0u, 0u, 0u, 0u};
     }
   }
   __syncthreads();
@@ -225,7 +217,7 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
     T* we = (T*)&w;
 #pragma unroll
     for (int e = 0; e < EPC; ++e) we[e] = Elem<T>::to(v[e]);
-    *(u32x4*)((T*)a.out + orow(p) * a.Cout + co) = w;
+    if (!(a.dbg & 32)) *(u32x4*)((T*)a.out + orow(p) * a.Cout + co) = w;
     if (a.stats) {
 #pragma unroll
       for (int q = 0; q < EPC / 4; ++q) {
@@ -236,7 +228,7 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
       }
     }
   }
-  if (a.stats) {
+  if (a.stats && !(a.dbg & 128)) {
     __syncthreads();
     const int Gt = stat_slot_px(HWo);  // host guarantees 128 % HWo == 0 or HWo % 128 == 0
     const int S = BN / Gt;
@@ -853,7 +845,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < GNC_ITEMS; ++j) {
       const T* p = src + (unsigned)(poff[j] * Cs + cs0);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 ? p : zero) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 && !(a.dbg & 64) ? p : zero) : "memory");
     }
     const f32x4* cp0 = (const f32x4*)(a.gn_coef + ((size_t)img0 * (Cin / 8) + cc * 8 + lch) * 16);
 #pragma unroll
@@ -899,29 +891,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
     if (a.dbg & 2) return;
     const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
     const char* A = wring + (s % GNC_NS) * TILEB;
-    // fragment reads two k-steps ahead of their MFMAs (see mma_stage)
-    bf16x8 af[4][2], bfg[4][2];
-    auto rd = [&](int kk) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[kk][i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 af[2], bfg[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int h = hb[j] + toff;
-        bfg[kk][j] = *(const bf16x8*)(halo + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
+        bfg[j] = *(const bf16x8*)(halo + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
       }
-    };
-    rd(0);
-    rd(1);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      if (kk + 2 < 4) rd(kk + 2);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfg[kk][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
   };
 
