@@ -132,7 +132,7 @@ def main():
             ops = nat.profile_ops(x, t)
         agg = {}
         for o in ops:
-            if o["kind"] in ("conv", "convgn"):
+            if o["kind"] in ("conv", "convgn", "convgnw", "convgnw4"):
                 g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
                 g[0] += 1
                 g[1] += o["ms"]
@@ -145,8 +145,10 @@ def main():
         total_ms = sum(o["ms"] for o in ops)
         conv_ms = sum(v[1] for v in agg.values())
         conv_fl = sum(v[2] for v in agg.values())
-        names = {"convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3)",
-                 "conv": "conv_pipe (implicit-GEMM conv)"}
+        names = {"convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3, 128x128 tile)",
+                 "convgnw": "conv3x3_gn_wide_kernel<1> (fused GroupNorm+SiLU+conv3x3, 128x256 tile)",
+                 "convgnw4": "conv3x3_gn_wide_kernel<4> (fused GroupNorm+SiLU+conv3x3, 8x8 level)",
+                 "conv": "conv_pipe_wide / conv_pipe / conv_small (implicit-GEMM conv)"}
         traffic = None
         tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kind}.json")
         if os.path.exists(tfile) and args.precision == "bf16" and n_local == 256:

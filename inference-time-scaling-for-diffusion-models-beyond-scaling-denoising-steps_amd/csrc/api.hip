@@ -35,6 +35,7 @@ hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hi
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
 bool conv_gn_eligible(int H, int W);
+int conv_gn_wide_segs(int H, int W, int M, int Cout);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
 hipError_t launch_tail_mfma(const TailArgs&, hipStream_t);
@@ -84,6 +85,8 @@ struct Act {
 
 enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF };
 constexpr int kCensusConvGN = 4;  // census kind of a fused GroupNorm+SiLU conv (conv3x3_gn_kernel)
+constexpr int kCensusConvGNW = 5;   // ... run as conv3x3_gn_wide_kernel<1>
+constexpr int kCensusConvGNW4 = 6;  // ... run as conv3x3_gn_wide_kernel<4>
 
 struct Op {
   OpKind kind;
@@ -757,9 +760,15 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   // census kinds: OpKind, and kCensusConvGN for the fused GroupNorm+SiLU convs
-  for (const Op& o : u->ops)
-    CHK(mark(o.kind == OP_CONV && o.coef != SIZE_MAX ? kCensusConvGN : (int)o.kind, op_flops(u, o, c.nb),
-             [&]() { return launch_op(u, o, c, s); }));
+  for (const Op& o : u->ops) {
+    int kind = (int)o.kind;
+    if (o.kind == OP_CONV && o.coef != SIZE_MAX) {
+      const Act& out = u->acts[o.dst];
+      const int segs = u->bf16 ? conv_gn_wide_segs(out.H, out.W, c.nb * out.H * out.W, o.Cout) : 0;
+      kind = segs == 1 ? kCensusConvGNW : segs == 4 ? kCensusConvGNW4 : kCensusConvGN;
+    }
+    CHK(mark(kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
+  }
   // tail GN + conv (+ sampler update); bf16 MFMA tail: GN coefficients, then one fused launch
   Op g;
   g.src1 = u->tail_in; g.gamma = u->tail_gn_g; g.beta = u->tail_gn_b; g.silu = 1;
@@ -872,6 +881,12 @@ int itsd_set_option(const char* key, int value) {
     // GN statistics pass, 256 no residual loads. (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
     itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256);
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {
+    // 256-pixel conv tiles (conv3x3_gn_wide_kernel / conv_pipe_wide): 0 off, 1 auto, 2 whenever eligible
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, std::string(key) + " in [0,2]");
+    (key[0] == 'g' ? itsd::g_gn_wide : itsd::g_conv_wide) = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
@@ -1114,7 +1129,10 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
     float ms = 0.f;
     if (r == ITSD_OK && e == hipSuccess) hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
     tm += ms;
-    if (kinds[i] == OP_CONV || kinds[i] == kCensusConvGN) { cm += ms; cf += fl[i]; ++cl; }
+    if (kinds[i] == OP_CONV || kinds[i] == kCensusConvGN || kinds[i] == kCensusConvGNW ||
+        kinds[i] == kCensusConvGNW4) {
+      cm += ms; cf += fl[i]; ++cl;
+    }
     hipEventDestroy(evs[i].first);
     hipEventDestroy(evs[i].second);
   }

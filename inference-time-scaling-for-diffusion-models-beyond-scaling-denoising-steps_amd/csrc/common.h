@@ -10,6 +10,8 @@ extern int g_conv_variant;  // kernel-variant switch for A/B measurements (itsd_
 extern int g_small_conv;   // 64x64-tile conv_small for small levels (itsd_set_option "small_conv")
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
+extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
+extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights

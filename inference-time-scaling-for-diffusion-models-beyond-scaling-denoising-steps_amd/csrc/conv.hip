@@ -42,6 +42,8 @@ int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
+int g_gn_wide = 0;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
+int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off, 1 auto, 2 whenever eligible
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -94,7 +96,7 @@ __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (
 // 3. per-channel (sum, sum of squares) over each pixel slot of the tile: the
 //    GroupNorm statistics of the consumer (Model.py:171,180), written as a
 //    deterministic partial slab stats[slot][2][Cout] (no atomics).
-template <typename T, int BM = 128, int BN = 128>
+template <typename T, int BM = 128, int BN = 128, int NTH = 256>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
 
 // accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
@@ -122,7 +124,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
 
 // E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
 // and the consumer GroupNorm's statistics slab.
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int NTH>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int ER = BM + 4;  // E row (floats): 128x128 tile -> EROW
@@ -180,7 +182,7 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
   constexpr int CPR = BM / EPC;  // 16-B output chunks per tile row
   const int cl = (tid % CPR) * EPC, co = tileC + cl;
   const int RPI = NT / CPR;       // rows per pass
-  constexpr int MAXR = (BN * CPR + 255) / 256;
+  constexpr int MAXR = (BN * CPR + NTH - 1) / NTH;  // NTH = blockDim.x
   // residual rows first: all loads in flight before the first use
   u32x4 rres[MAXR];
   if (a.resid) {
@@ -963,6 +965,356 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
+// ---------------------------------------------------------------------------- 256-pixel tiles
+// The census of the 128 x 128 kernels with their measurement switches (itsd_set_option
+// "conv_dbg") showed their loops bound by the per-stage operand stream and its latency, not
+// by the matrix pipe: with the MFMAs skipped, conv3x3_gn_kernel still took 62 % of its time.
+// The kernels below take a 128 couts x 256 pixels tile with 8 waves (2 cout halves x 4 pixel
+// quarters of 64 x 64) sharing every stage -- twice the MFMAs per streamed weight byte -- and
+// one block owns the CU's 160 KiB of LDS, so the ring keeps more stages in flight. Per output,
+// the MFMA sequence (tap, channel chunk, k) and the epilogue are the 128-pixel kernels', so
+// without a K split the results are bit-identical to theirs.
+constexpr int GNW_BN = 256;                                                   // pixels per tile
+constexpr int GNW_EPI = GNW_BN * EROW * 4 + (GNW_BN / 16) * 2 * CONV_BM * 4;  // E tile + statistics groups
+constexpr int GNW_SMEM = 160 * 1024;
+static_assert(GNW_EPI <= GNW_SMEM, "epilogue tile");
+
+// accumulators of the 8 waves (2 x 4 of 64 x 64) -> E[pixel][cout] (256 x 128 fp32)
+__device__ __forceinline__ void acc_to_E_wide(f32x16 (&acc)[2][2], float* E) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
+      }
+}
+
+// Fused GroupNorm+SiLU+conv3x3 (conv3x3_gn_kernel's work, Model.py:170-174,179-184) at 256
+// pixels: 8 rows of a 32x32 image or a whole 16x16 image (NSEG = 1), four 8x8 images (NSEG = 4).
+//   * weight ring NS deep: NS-1 stages in flight across the raw barriers;
+//   * double-buffered halo: the next chunk's GroupNorm+SiLU transform is spread over taps
+//     NS..8, one 64-row item per tap, beside the other waves' MFMAs, instead of a block-wide
+//     transform phase between chunks;
+//   * halo rows of image segment g (HS = (rows + 2)(W + 2) each) start at g*HS; a thread
+//     stages rows of one segment only (one image's GN coefficients in registers); its rows
+//     past HS are scratch rows behind all segments.
+template <int NSEG> struct GnwCfg;
+template <> struct GnwCfg<1> { static constexpr int ITEMS = 6, NS = 4; };  // 2 x 48 KiB halo + 4 x 16 KiB ring
+template <> struct GnwCfg<4> { static constexpr int ITEMS = 7, NS = 3; };  // 2 x 56 KiB halo + 3 x 16 KiB ring
+static_assert(2 * GnwCfg<1>::ITEMS * 64 * ROWB + GnwCfg<1>::NS * TILEB <= GNW_SMEM, "LDS");
+static_assert(2 * GnwCfg<4>::ITEMS * 64 * ROWB + GnwCfg<4>::NS * TILEB <= GNW_SMEM, "LDS");
+
+template <int NSEG>
+__global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int ITEMS = GnwCfg<NSEG>::ITEMS, NS = GnwCfg<NSEG>::NS;
+  constexpr int LPC = ITEMS + 4;                  // vector loads per lane per chunk: halo items + coefficients
+  constexpr int HALO = ITEMS * 64 * ROWB;         // one halo buffer
+  constexpr int TPS = 512 / NSEG, RPP = TPS / 8;  // threads per image segment, its halo rows per pass
+  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
+  char* wring = smem + 2 * HALO;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
+  const int H = a.Hout, W = a.Wout, HW = H * W, W2 = W + 2;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64, nS = 9 * ncc;
+  const int THs = NSEG == 1 ? GNW_BN / W : H;  // output rows of one segment
+  const int HS = (THs + 2) * W2;
+  const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
+  const T* zero = zero_of_block<T>(a);
+
+  int hb[2];  // halo row of this lane's B columns at tap (0,0)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pl = wn * 64 + j * 32 + rl;
+    const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
+    hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+  }
+  int arow[2];  // weight rows: DMA q of wave w fills rows 8*(2w+q) .. +7 of the stage
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * (2 * wid + q) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int co = tileC + r;
+    arow[q] = co < a.Cout ? co * a.K + c * 8 : -1;
+  }
+  const int lch = tid & 7, sg = tid / TPS, lt = tid - sg * TPS;
+  int hrow[ITEMS], poff[ITEMS];  // LDS halo row of item j; its input pixel, or -1 (padding / scratch)
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int r = (lt >> 3) + RPP * j;
+    hrow[j] = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
+    int po = -1;
+    if (r < HS) {
+      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) po = ((img0 + sg) * H + iy) * W + ix;
+    }
+    poff[j] = po;
+  }
+  // every step issues exactly 2 weight DMAs per wave (zero page past the last stage)
+  auto issue_w = [&](int s) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const int k0 = tap * Cin + cc * 64;
+    char* dst = wring + (s % NS) * TILEB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const T* ga = (arow[q] >= 0 && s < nS) ? (const T*)a.wt + (unsigned)(arow[q] + k0) : zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(dst + (2 * wid + q) * 1024), 16, 0, 0);
+    }
+  };
+  f32x16 acc[2][2];
+  u32x4 hreg[ITEMS];
+  f32x4 cf[4];  // a[8], b[8] of this lane's 8 channels for its segment's image
+  // halo + coefficient loads as inline asm (outside hipcc's vmcnt bookkeeping, which would
+  // drain the weight DMAs); the counted waits of the tap loop retire them
+  auto load_chunk = [&](int cc) {
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int Cs = s1 ? a.C1 : a.C2;
+    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const T* p = src + (unsigned)(poff[j] * Cs + cs0);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 ? p : zero) : "memory");
+    }
+    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cf[q]) : "v"(cp + q) : "memory");
+  };
+  // item j -> silu(x*a + b) as bf16 (padding exactly 0); called only after the counted wait
+  // that retired the chunk's loads: the empty asm keeps every consumer below that point
+  auto write_item = [&](char* hbuf, int j) {
+    asm volatile("" : "+v"(hreg[j]), "+v"(cf[0]), "+v"(cf[1]), "+v"(cf[2]), "+v"(cf[3]));
+    const uint32_t* xw = (const uint32_t*)&hreg[j];
+    u32x4 y;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
+      const f32x2 x = {__uint_as_float(xw[w] << 16), __uint_as_float(xw[w] & 0xffff0000u)};
+      const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
+      const f32x2 sc = (w & 1) ? f32x2{av[2], av[3]} : f32x2{av[0], av[1]};
+      const f32x2 sh = (w & 1) ? f32x2{bv[2], bv[3]} : f32x2{bv[0], bv[1]};
+      const f32x2 r = gn_silu2(x, sc, sh);
+      y[w] = (uint32_t)f2bf(r.x) | ((uint32_t)f2bf(r.y) << 16);
+    }
+    const bool pad = poff[j] < 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
+    const int h = hrow[j];
+    *(u32x4*)(hbuf + h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4)) = y;
+  };
+  auto mma_tap = [&](const char* hbuf, int s, int tap) {
+    const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
+    const char* A = wring + (s % NS) * TILEB;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 af[2], bfg[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int h = hb[j] + toff;
+        bfg[j] = *(const bf16x8*)(hbuf + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  zero_acc(acc);
+  load_chunk(0);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue_w(s);
+  wait_vmcnt<2 * (NS - 1)>();  // the chunk-0 loads (older than the weight DMAs)
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) write_item(smem, j);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // One chunk = 9 taps. Step s waits for its weight stage with the NS-2 younger stages (2 DMAs
+  // each) left in flight -- plus, at taps 1..NS-1, the next chunk's LPC loads issued at tap 0 --
+  // passes the barrier, refills the ring slot read at step s-1 and runs its MFMAs. The last
+  // three taps (peeled: item indices must be compile-time) also write the next chunk's halo,
+  // a third of the items each; taps 1-5 are a runtime loop (a fully unrolled chunk spills).
+  constexpr int TW = 6;
+  static_assert(TW >= NS, "the chunk's loads are retired before the first item write");
+  auto step = [&](int s0, int tap, const char* hcur, bool lpc_in_flight) {
+    if (lpc_in_flight) wait_vmcnt<2 * (NS - 2) + LPC>();
+    else wait_vmcnt<2 * (NS - 2)>();
+    __builtin_amdgcn_s_barrier();
+    issue_w(s0 + tap + NS - 1);
+  };
+  auto run_chunk = [&](int cc, auto stage) {
+    constexpr bool ST = decltype(stage)::value;
+    const int s0 = cc * 9;
+    const char* hcur = smem + (cc & 1) * HALO;
+    char* hnext = smem + ((cc + 1) & 1) * HALO;
+    step(s0, 0, hcur, false);
+    if constexpr (ST) {
+      asm volatile("" ::: "memory");
+      load_chunk(cc + 1);
+      asm volatile("" ::: "memory");
+    }
+    mma_tap(hcur, s0, 0);
+#pragma unroll 1
+    for (int tap = 1; tap < TW; ++tap) {
+      step(s0, tap, hcur, ST && tap <= NS - 1);
+      mma_tap(hcur, s0 + tap, tap);
+    }
+#pragma unroll
+    for (int k = 0; k < 9 - TW; ++k) {
+      step(s0, TW + k, hcur, false);
+      mma_tap(hcur, s0 + TW + k, TW + k);
+      if constexpr (ST) {
+#pragma unroll
+        for (int j = k * ITEMS / 3; j < (k + 1) * ITEMS / 3; ++j) write_item(hnext, j);
+      }
+    }
+    if constexpr (ST) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
+  run_chunk(ncc - 1, std::false_type{});
+  wait_vmcnt<0>();
+  __syncthreads();
+  acc_to_E_wide(acc, (float*)smem);
+  __syncthreads();
+  epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
+}
+
+// Plain implicit-GEMM conv (conv_pipe's work: 3x3 stride 2, the 4x4 level's 3x3s, 1x1s) at
+// 256 pixels: each 48 KiB stage (16 KiB of weights + 32 KiB of gathered pixel rows, both by
+// global_load_lds) through a 3-deep ring, 2 stages in flight. Under-filled grids split K over
+// gridDim.z: slices store fp32 partial tiles and splitk_wide_epilogue_kernel sums them in
+// slice order (deterministic).
+constexpr int CPW_NS = 3, CPW_STAGE = 3 * TILEB;
+constexpr int CPW_SMEM = CPW_NS * CPW_STAGE > GNW_EPI ? CPW_NS * CPW_STAGE : GNW_EPI;
+static_assert(CPW_SMEM <= GNW_SMEM, "LDS");
+
+__global__ __launch_bounds__(512, 1) void conv_pipe_wide(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int NS = CPW_NS, BK = 64;
+  __shared__ __attribute__((aligned(16))) char smem[CPW_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
+  const int Cin = a.C1 + a.C2, cpt = Cin / BK, nK = a.ksize * a.ksize * cpt;
+  const int HWo = a.Hout * a.Wout;
+  const T* zero = zero_of_block<T>(a);
+  // DMA rows: weights, instruction q of wave w -> rows 8*(2w+q) ..; pixels -> rows 8*(4w+q) ..
+  const T* arow[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * (2 * wid + q) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int co = tileC + r;
+    arow[q] = co < a.Cout ? (const T*)a.wt + (size_t)co * a.K + c * 8 : nullptr;
+  }
+  int pix1[4], pix2[4];
+  unsigned tmask[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 8 * (4 * wid + q) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int p = tileP + r;
+    const bool pv = p < a.M;
+    const int img = p / HWo, rem = p - img * HWo, oy = rem / a.Wout;
+    const int iy0 = oy * a.stride - a.pad, ix0 = (rem - oy * a.Wout) * a.stride - a.pad;
+    const int pl = (img * a.Hin + iy0) * a.Win + ix0;
+    pix1[q] = pl * a.C1 + c * 8;
+    pix2[q] = pl * a.C2 + c * 8;
+    unsigned m = 0;
+    for (int ky = 0; ky < a.ksize; ++ky)
+      for (int kx = 0; kx < a.ksize; ++kx) {
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        if (pv && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win) m |= 1u << (ky * a.ksize + kx);
+      }
+    tmask[q] = m;
+  }
+  auto issue = [&](int kc) {
+    const int tap = kc / cpt, ci0 = (kc - tap * cpt) * BK;
+    const int ky = tap / a.ksize, kx = tap - ky * a.ksize;
+    char* sA = smem + (kc % NS) * CPW_STAGE;
+    char* sB = sA + TILEB;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int toff = (ky * a.Win + kx) * (s1 ? a.C1 : a.C2) + (s1 ? ci0 : ci0 - a.C1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const T* ga = arow[q] ? arow[q] + (size_t)kc * BK : zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sA + (2 * wid + q) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const T* gb = ((tmask[q] >> tap) & 1u) ? src + (s1 ? pix1[q] : pix2[q]) + toff : zero;
+      __builtin_amdgcn_global_load_lds((const void*)gb, (lds_ptr_t)(sB + (4 * wid + q) * 1024), 16, 0, 0);
+    }
+  };
+  f32x16 acc[2][2];
+  zero_acc(acc);
+  const int S = gridDim.z, z = bt.z;
+  const int k0 = (int)((long long)nK * z / S), k1 = (int)((long long)nK * (z + 1) / S);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (k0 + s < k1) issue(k0 + s);
+  for (int kc = k0; kc < k1; ++kc) {
+    if (kc + 1 < k1) wait_vmcnt<6>();  // the one younger stage (6 DMAs per wave) stays in flight
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kc + NS - 1 < k1) issue(kc + NS - 1);
+    const char* A = smem + (kc % NS) * CPW_STAGE;
+    mma_stage<T>(A, A + TILEB, acc, wm, wn, rl, hh);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  if (S > 1) {  // partial tile: slab[tile][slice][thread][64]
+    float* mine = a.splitk_ws + (((size_t)bt.y * gridDim.x + bt.x) * S + z) * 32768 + tid * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          *(f32x4*)(mine + (i * 2 + j) * 16 + 4 * g) = v;
+        }
+    return;
+  }
+  acc_to_E_wide(acc, (float*)smem);
+  __syncthreads();
+  epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
+}
+
+__global__ __launch_bounds__(512, 1) void splitk_wide_epilogue_kernel(ConvArgs a, int S) {
+  __shared__ __attribute__((aligned(16))) char smem[GNW_EPI];
+  const int tileP = blockIdx.x * GNW_BN, tileC = blockIdx.y * CONV_BM;
+  const float* src = a.splitk_ws + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * S * 32768 + threadIdx.x * 64;
+  f32x16 acc[2][2];
+  zero_acc(acc);
+  for (int z = 0; z < S; ++z, src += 32768) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *(const f32x4*)(src + (i * 2 + j) * 16 + 4 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
+        }
+  }
+  acc_to_E_wide(acc, (float*)smem);
+  __syncthreads();
+  epilogue_from_E<bf16_t, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
+}
+
 // GroupNorm finalize for the fused conv (the statistics half of gn_apply_kernel): per
 // image the group mean / rstd in fp64 from the producers' slabs, then per channel
 // a = rstd*gamma, b = beta - mean*a as coef[img][C/8][a0..a7, b0..b7].
@@ -1116,10 +1468,62 @@ bool conv_gn_eligible(int H, int W) {
   return segs <= 2 && segs * (THs + 2) * (W + 2) <= GNC_HALO_ROWS;
 }
 
+// Which fused GroupNorm conv launch_conv runs at this shape: 0 = conv3x3_gn_kernel (128 x 128),
+// 1 / 4 = conv3x3_gn_wide_kernel<1 | 4> (256 pixels = rows of one image | four 8x8 images).
+int conv_gn_wide_segs(int H, int W, int M, int Cout) {
+  if (!g_gn_wide || W > GNW_BN || GNW_BN % W || M % GNW_BN) return 0;
+  int segs = 0;
+  if (GNW_BN / W <= H) {
+    const int THs = GNW_BN / W;
+    if (H % THs == 0 && (THs + 2) * (W + 2) <= GnwCfg<1>::ITEMS * 64) segs = 1;
+  } else if (GNW_BN == 4 * H * W && (H + 2) * (W + 2) <= GnwCfg<4>::ITEMS * 16) {
+    segs = 4;
+  }
+  const long long blocks = (long long)(M / GNW_BN) * ((Cout + CONV_BM - 1) / CONV_BM);
+  return segs && (g_gn_wide == 2 || blocks >= 192) ? segs : 0;
+}
+
+// conv_pipe_wide for plain bf16 convs in whole 64-channel K-chunks whose 256-pixel tiles hold
+// whole images or whole GroupNorm statistics slots. Auto: at least 12 K-stages (short-K 1x1s
+// stay on the 2-blocks-per-CU conv_pipe) and ~one block per CU (split K below that). Returns
+// true when it launched (*err set).
+static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) {
+  if (!g_conv_wide) return false;
+  const int HWo = a.Hout * a.Wout, Cin = a.C1 + a.C2;
+  if (!a.zero || a.subpix || a.upsample || a.zins || a.gn_coef || Cin % 64 || a.C1 % 64 || a.Cout % 8 ||
+      a.K != a.ksize * a.ksize * Cin || a.ksize > 5 || (HWo % GNW_BN && GNW_BN % HWo) || (HWo % 128 && 128 % HWo) ||
+      (a.vt_out && HWo % 8))
+    return false;
+  dim3 grid((a.M + GNW_BN - 1) / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+  const int blocks = (int)(grid.x * grid.y), nK = a.ksize * a.ksize * (Cin / 64);
+  if (g_conv_wide != 2 && nK < 12) return false;
+  int S = 1;
+  if (blocks < 192 && a.splitk_ws && g_splitk) {  // under-filled: about one block per CU, >= 8 stages a slice
+    S = std::min((256 + blocks - 1) / blocks, nK / 8);
+    while (S > 1 && (long long)blocks * S * 32768 > a.splitk_cap) --S;
+    if (S < 1) S = 1;
+  }
+  if (g_conv_wide != 2 && blocks * S < 192) return false;
+  grid.z = S;
+  hipLaunchKernelGGL(conv_pipe_wide, grid, dim3(512), 0, s, a);
+  *err = hipGetLastError();
+  if (*err == hipSuccess && S > 1) {
+    hipLaunchKernelGGL(splitk_wide_epilogue_kernel, dim3(grid.x, grid.y), dim3(512), 0, s, a, S);
+    *err = hipGetLastError();
+  }
+  return true;
+}
+
 template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (a.gn_coef) {
+      if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
+        const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+        if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
+        return hipGetLastError();
+      }
       dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
       const int THs = std::min(a.Hout, 128 / a.Wout), segs = 128 / (THs * a.Wout);
       if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_kernel<1>, grid, dim3(256), 0, s, a);
@@ -1129,6 +1533,10 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   }
   constexpr int BK = 8 * (16 / (int)sizeof(T));
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+  if constexpr (sizeof(T) == 2) {
+    hipError_t we;
+    if (conv_wide_launch(a, s, &we)) return we;
+  }
   if constexpr (sizeof(T) == 2) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
@@ -1147,7 +1555,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
-  if (pipe && v == 2 && a.splitk_ws && g_splitk) {
+  if (pipe && v != 1 && a.splitk_ws && g_splitk) {
     // under-filled grids (the 8x8 / 4x4 levels): split K so that >= ~2 blocks per CU exist,
     // keeping >= 8 K-stages per slice
     const int blocks = (int)(grid.x * grid.y);
@@ -1161,7 +1569,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if (!pipe || v == 1) hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
   else if (v == 2 && lin) hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
   else if (v == 2) hipLaunchKernelGGL((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
+  else if (v == 3 && lin) hipLaunchKernelGGL((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
   else if (v == 3) hipLaunchKernelGGL((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
+  else if (lin) hipLaunchKernelGGL((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
   if (grid.z > 1) {
     hipError_t e = hipGetLastError();

@@ -191,7 +191,7 @@ class NativeUNet:
                                      kinds.ctypes.data, ms.ctypes.data, fl.ctypes.data, sh.ctypes.data,
                                      ctypes.byref(n), stream_ptr(x.device)))
         k = n.value
-        names = {0: "gn", 1: "conv", 2: "attn", 3: "gncoef", 4: "convgn", -1: "head", -2: "tail"}
+        names = {0: "gn", 1: "conv", 2: "attn", 3: "gncoef", 4: "convgn", 5: "convgnw", 6: "convgnw4", -1: "head", -2: "tail"}
         return [{"kind": names.get(int(kinds[i]), str(kinds[i])), "ms": float(ms[i]), "flops": float(fl[i]),
                  "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
                  "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5])} for i in range(k)]

@@ -283,3 +283,72 @@ def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt):
     else:  # P and the output are rounded to bf16
         assert _rel_l2(out, ref) < 1e-2
         assert (out - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+
+
+_TILE_DEFAULTS = {"gn_wide": 0, "conv_wide": 0, "splitk": 1}
+
+
+def _eps_with(net, x, t, **opts):
+    """eps of one forward under itsd_set_option overrides (the defaults restored after)."""
+    try:
+        for k, v in opts.items():
+            rt.set_option(k, v)
+        return net(x, t).cpu()
+    finally:
+        for k, v in _TILE_DEFAULTS.items():
+            rt.set_option(k, v)
+
+
+@pytest.mark.parametrize("n", [8, 12])
+def test_wide_tile_convs_bit_identical_and_vs_oracle(n):
+    """The 256-pixel kernels forced on (conv3x3_gn_wide_kernel: rows of one 32x32 / 16x16
+    image, four 8x8 images; conv_pipe_wide: the plain convs) reproduce the 128-pixel kernels
+    bit for bit when K is not split (same MFMA order per output, same epilogue); with the
+    small levels' split-K they stay within the bf16 tolerance of the oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(200 + n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    xd, td = x.cuda(), t.cuda()
+    narrow = _eps_with(net, xd, td, gn_wide=0, conv_wide=0, splitk=0)
+    wide = _eps_with(net, xd, td, gn_wide=2, conv_wide=2, splitk=0)
+    assert torch.equal(narrow, wide)
+    again = _eps_with(net, xd, td, gn_wide=2, conv_wide=2, splitk=0)
+    assert torch.equal(wide, again)
+    wide_sk = _eps_with(net, xd, td, gn_wide=2, conv_wide=2, splitk=1)
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x, t)
+    assert _rel_l2(wide, ref) < REL_L2_BF16
+    assert _rel_l2(wide_sk, ref) < REL_L2_BF16
+
+
+def test_wide_tile_convs_full_batch_bit_identical():
+    """At the bench batch (N = 256, where the automatic choice takes the 256-pixel kernels)
+    the forward equals the 128-pixel kernels' bit for bit (K unsplit on both sides)."""
+    net = _net(ARCH_A, "bf16")
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(256, 3, 32, 32, generator=gen).cuda()
+    t = torch.randint(0, 1000, (256,), generator=gen).cuda()
+    narrow = _eps_with(net, x, t, gn_wide=0, conv_wide=0, splitk=0)
+    auto = _eps_with(net, x, t, gn_wide=1, conv_wide=1, splitk=0)
+    assert torch.equal(narrow, auto)
+    assert torch.isfinite(auto).all()
+
+
+def test_wide_tile_convs_cfg_bit_identical():
+    """CFG UNet (C3 arch, 512-channel 16x16 level: four cout tiles) on the reference fixture
+    input: 256-pixel kernels forced on == 128-pixel kernels, bit for bit."""
+    g = golden("archC_eps")
+    net = _net(ARCH_C, "bf16")
+    x, t, lab = (torch.from_numpy(g[k]).cuda() for k in ("x", "t", "labels"))
+    outs = []
+    for opts in ({"gn_wide": 0, "conv_wide": 0, "splitk": 0}, {"gn_wide": 2, "conv_wide": 2, "splitk": 0}):
+        try:
+            for k, v in opts.items():
+                rt.set_option(k, v)
+            outs.append(net(x, t, lab).cpu())
+        finally:
+            for k, v in _TILE_DEFAULTS.items():
+                rt.set_option(k, v)
+    assert torch.equal(outs[0], outs[1])

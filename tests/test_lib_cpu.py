@@ -69,3 +69,18 @@ def test_reference_noise_plan_order():
         for k, t in enumerate([3, 2, 1]):
             assert torch.equal(noise[t, run], seq[4 * run + 1 + k][0])
     assert torch.count_nonzero(noise[0]) == 0
+
+
+def test_conv_tile_options():
+    """The conv tile switches (itsd_set_option) accept 0 off / 1 auto / 2 whenever eligible and
+    reject other values; host-side only (no device call)."""
+    if not os.path.exists(rt.LIB_PATH):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    for key, default in (("gn_wide", 0), ("conv_wide", 0), ("small_conv", 1)):
+        for v in (0, 1, 2):
+            rt.set_option(key, v)
+        with pytest.raises(rt.ItsdError):
+            rt.set_option(key, 3)
+        rt.set_option(key, default)

@@ -13,6 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 import itsd
+
+CONV_KINDS = ("conv", "convgn", "convgnw", "convgnw4")
 from itsd.arch import ARCH_A
 from itsd.model import UNet
 
@@ -39,7 +41,7 @@ def main():
     if args.variants:
         # each variant: '+'-joined itsd_set_option key=value pairs, e.g.
         # "base", "small_conv=0", "conv_variant=2+splitk=0", "conv_dbg=19"
-        defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1}
+        defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1, "gn_wide": 0, "conv_wide": 0}
         for rnd in range(3):
             for v in args.variants.split(","):
                 opts = dict(defaults)
@@ -50,7 +52,7 @@ def main():
                 for k, val in opts.items():
                     rt.set_option(k, val)
                 ops = nat.profile_ops(x, t)
-                conv = [o for o in ops if o["kind"] in ("conv", "convgn")]
+                conv = [o for o in ops if o["kind"] in CONV_KINDS]
                 by = defaultdict(lambda: [0.0, 0.0])
                 for o in conv:
                     by[o["H"]][0] += o["ms"]
@@ -68,7 +70,7 @@ def main():
         tf = o["flops"] / (o["ms"] * 1e-3) / 1e12 if o["ms"] > 0 and o["flops"] > 0 else 0.0
         print(f"{i:3d} {o['kind']:5} {o['M']:7d} {o['N']:5d} {o['K']:5d} {o['H']:3d} {o['ks']:2d} {o['stride_up']:3d} "
               f"{o['ms']:8.4f} {tf:7.1f}")
-        key = o["kind"] if o["kind"] not in ("conv", "convgn") else f"{o['kind']} H{o['H']}"
+        key = o["kind"] if o["kind"] not in CONV_KINDS else f"{o['kind']} H{o['H']}"
         agg[key][0] += 1
         agg[key][1] += o["ms"]
         agg[key][2] += o["flops"]

@@ -3,6 +3,7 @@ mkdir -p gpurun_out/r01 profiles
 timeout -k 10 600 bash tools/pmc_passes.sh gpurun_out/r01/pmc --n 256 > gpurun_out/r01/pmc.log 2>&1 || { echo pmc_fail; exit 1; }
 python tools/pmc_traffic.py gpurun_out/r01/pmc convgn profiles/pmc_traffic_convgn.json > gpurun_out/r01/traffic_convgn.json || exit 1
 python tools/pmc_traffic.py gpurun_out/r01/pmc conv profiles/pmc_traffic_conv.json > gpurun_out/r01/traffic_conv.json || exit 1
+python tools/pmc_traffic.py gpurun_out/r01/pmc convgnw profiles/pmc_traffic_convgnw.json > gpurun_out/r01/traffic_convgnw.json || exit 1
 cp profiles/pmc_traffic_*.json gpurun_out/r01/
 timeout -k 10 600 python bench.py > gpurun_out/r01/bench.json 2> gpurun_out/r01/bench.err || { echo bench_fail; tail -5 gpurun_out/r01/bench.err; exit 1; }
 cat gpurun_out/r01/bench.json

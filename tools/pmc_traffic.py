@@ -15,7 +15,9 @@ from collections import defaultdict
 
 FAMILIES = {
     "convgn": ("conv3x3_gn_kernel",),
-    "conv": ("conv_pipe", "splitk_epilogue_kernel"),
+    "convgnw": ("conv3x3_gn_wide_kernel<1>", "conv3x3_gn_wide_kernelILi1E"),
+    "convgnw4": ("conv3x3_gn_wide_kernel<4>", "conv3x3_gn_wide_kernelILi4E"),
+    "conv": ("conv_pipe", "conv_small", "splitk_epilogue_kernel", "splitk_wide_epilogue_kernel"),
 }
 
 
