@@ -878,9 +878,10 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "conv_dbg")) {  // measurements only (results are wrong when set): 1 no
     // in-loop loads (zero-page sources), 2 no MFMA, 8 no GN transform, 16 no epilogue,
     // 32 no epilogue output stores, 64 fused-conv halo loads from the zero page, 128 no
-    // GN statistics pass, 256 no residual loads. (Never skip an issued load's wait: an
+    // GN statistics pass, 256 no residual loads, 512 (wide fused
+    // conv) s_setprio 1 for waves 4-7 (results unchanged). (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
-    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256);
+    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512);
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {

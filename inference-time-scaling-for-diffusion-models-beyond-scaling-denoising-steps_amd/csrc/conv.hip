@@ -42,8 +42,9 @@ int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
-int g_gn_wide = 0;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
-int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off, 1 auto, 2 whenever eligible
+int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
+int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
+                         // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -1028,6 +1029,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
   const int HS = (THs + 2) * W2;
   const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
   const T* zero = zero_of_block<T>(a);
+  // measurement switch 512: static priority for the second-dispatched half (waves 4-7)
+  if ((a.dbg & 512) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   int hb[2];  // halo row of this lane's B columns at tap (0,0)
 #pragma unroll
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
     char* dst = wring + (s % NS) * TILEB;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const T* ga = (arow[q] >= 0 && s < nS) ? (const T*)a.wt + (unsigned)(arow[q] + k0) : zero;
+      const T* ga = (arow[q] >= 0 && s < nS && (s < NS - 1 || !(a.dbg & 1))) ? (const T*)a.wt + (unsigned)(arow[q] + k0) : zero;
       __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(dst + (2 * wid + q) * 1024), 16, 0, 0);
     }
   };
@@ -1082,7 +1085,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const T* p = src + (unsigned)(poff[j] * Cs + cs0);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 ? p : zero) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 && !(a.dbg & 64) ? p : zero) : "memory");
     }
     const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
 #pragma unroll
@@ -1093,9 +1096,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
   auto write_item = [&](char* hbuf, int j) {
     asm volatile("" : "+v"(hreg[j]), "+v"(cf[0]), "+v"(cf[1]), "+v"(cf[2]), "+v"(cf[3]));
     const uint32_t* xw = (const uint32_t*)&hreg[j];
-    u32x4 y;
+    u32x4 y = hreg[j];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
+      if (a.dbg & 8) break;
       const f32x2 x = {__uint_as_float(xw[w] << 16), __uint_as_float(xw[w] & 0xffff0000u)};
       const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
       const f32x2 sc = (w & 1) ? f32x2{av[2], av[3]} : f32x2{av[0], av[1]};
@@ -1110,6 +1114,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
     *(u32x4*)(hbuf + h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4)) = y;
   };
   auto mma_tap = [&](const char* hbuf, int s, int tap) {
+    if (a.dbg & 2) return;
     const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
     const char* A = wring + (s % NS) * TILEB;
 #pragma unroll
@@ -1183,6 +1188,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
   run_chunk(ncc - 1, std::false_type{});
   wait_vmcnt<0>();
   __syncthreads();
+  if (a.dbg & 16) return;
   acc_to_E_wide(acc, (float*)smem);
   __syncthreads();
   epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);

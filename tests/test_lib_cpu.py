@@ -78,7 +78,7 @@ def test_conv_tile_options():
         import __graft_entry__
 
         __graft_entry__.build()
-    for key, default in (("gn_wide", 0), ("conv_wide", 0), ("small_conv", 1)):
+    for key, default in (("gn_wide", 1), ("conv_wide", 0), ("small_conv", 1)):
         for v in (0, 1, 2):
             rt.set_option(key, v)
         with pytest.raises(rt.ItsdError):

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
     ap.add_argument("--fuse-gn", type=int, default=1, help="fused GroupNorm+SiLU+conv3x3 in ResBlocks")
     ap.add_argument("--io-mfma", type=int, default=1, help="bf16 head/tail on MFMA (tail GroupNorm fused)")
+    ap.add_argument("--set", default="", help="itsd_set_option overrides for the final table, e.g. gn_wide=1+conv_dbg=2")
     args = ap.parse_args()
     from itsd import runtime as rt
     rt.set_option("fuse_gn", args.fuse_gn)
@@ -41,7 +42,7 @@ def main():
     if args.variants:
         # each variant: '+'-joined itsd_set_option key=value pairs, e.g.
         # "base", "small_conv=0", "conv_variant=2+splitk=0", "conv_dbg=19"
-        defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1, "gn_wide": 0, "conv_wide": 0}
+        defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1, "gn_wide": 1, "conv_wide": 0}
         for rnd in range(3):
             for v in args.variants.split(","):
                 opts = dict(defaults)
@@ -61,6 +62,9 @@ def main():
                       + " ".join(f"H{h}:{m:.3f}ms/{f / m / 1e9:.0f}TF" for h, (m, f) in sorted(by.items())))
         for k, val in defaults.items():
             rt.set_option(k, val)
+    for kv in filter(None, args.set.split("+")):
+        k, val = kv.split("=")
+        rt.set_option(k, int(val))
     for _ in range(args.reps):
         ops = nat.profile_ops(x, t)
     tot = sum(o["ms"] for o in ops)
