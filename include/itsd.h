@@ -138,8 +138,17 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
                      double* ms, double* flops, int* shapes, int* n_ops, void* stream);
 
-/* Process-wide tuning switches for A/B measurements. Keys: "conv_variant"
- * (0 = default: DMA-ring conv, 4 stages; 1 = register-staged; 2/3 = DMA ring, 2/3 stages). */
+/* Steady-state duration of one program op (synchronous): runs one forward at batch n to set up
+ * its inputs, then launches op `op_index` (census numbering of itsd_profile_ops: 1 = first
+ * program op) `reps` times back to back between two HIP events on the UNet's stream;
+ * *ms = elapsed / reps. The per-launch time a replayed step graph sees, without the eager
+ * census's per-launch event overhead. */
+int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int op_index, int reps, double* ms,
+                    void* stream);
+
+/* Process-wide switches for A/B measurements (api.hip lists every key): kernel variants and
+ * tile choices ("conv_variant", "splitk", "small_conv", "gn_wide", "conv_wide", "fuse_gn",
+ * "io_mfma") and measurement-only ablations ("conv_dbg"). */
 int itsd_set_option(const char* key, int value);
 
 const char* itsd_last_error(void);

@@ -1147,6 +1147,44 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
   return ITSD_OK;
 }
 
+int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int op_index, int reps, double* ms,
+                    void* stream) {
+  if (!u || !x || !t || !ms || reps < 1) return fail(ITSD_ERR_INVALID, "null argument or reps < 1");
+  if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_op: DDPM only");
+  if (op_index < 1 || op_index > (int)u->ops.size()) return fail(ITSD_ERR_INVALID, "profile_op: op_index out of range");
+  CHK(check_batch(u, n));
+  HIPCHK(hipSetDevice(u->device));
+  hipStream_t s = u->stream;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  float* eps = nullptr;
+  HIPCHK(hipMalloc(&eps, (size_t)n * 3 * u->H * u->H * 4));
+  int r = temb_rows(u, t, n, 0, false, u->proj_buf, s);
+  RunCtx c{};
+  c.nb = n; c.x = x; c.x_mod = n;
+  c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
+  c.label_mod = n; c.uncond_from = -1;
+  c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
+  if (r == ITSD_OK) r = run_program(u, c, s);  // every op's inputs in place
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  const Op& o = u->ops[op_index - 1];
+  if (r == ITSD_OK && e == hipSuccess) r = launch_op(u, o, c, s);  // warm
+  if (r == ITSD_OK && e == hipSuccess) e = hipEventRecord(e0, s);
+  for (int i = 0; i < reps && r == ITSD_OK && e == hipSuccess; ++i) r = launch_op(u, o, c, s);
+  if (r == ITSD_OK && e == hipSuccess) e = hipEventRecord(e1, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  float m = 0.f;
+  if (r == ITSD_OK && e == hipSuccess) e = hipEventElapsedTime(&m, e0, e1);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(eps);
+  CHK(r);
+  HIPCHK(e);
+  *ms = (double)m / reps;
+  return ITSD_OK;
+}
+
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds, double* ms,
                      double* flops, int* shapes, int* n_ops, void* stream) {
   if (!u || !x || !t || !n_ops) return fail(ITSD_ERR_INVALID, "null argument");

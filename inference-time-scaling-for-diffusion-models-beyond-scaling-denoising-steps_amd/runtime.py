@@ -62,6 +62,8 @@ _SIGS = {
     "itsd_profile_forward": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double), ctypes.c_void_p],
+    "itsd_profile_op": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                        ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p],
     "itsd_profile_ops": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
@@ -178,6 +180,13 @@ class NativeUNet:
         check(lib().itsd_profile_forward(self.h, x.data_ptr(), t.data_ptr(), x.shape[0], ctypes.byref(cm),
                                          ctypes.byref(cf), ctypes.byref(cl), ctypes.byref(tm), stream_ptr(x.device)))
         return {"conv_ms": cm.value, "conv_flops": cf.value, "conv_launches": cl.value, "total_ms": tm.value}
+
+    def profile_op(self, x: torch.Tensor, t: torch.Tensor, op_index: int, reps: int = 10) -> float:
+        """Steady-state ms of program op `op_index` (profile_ops numbering), `reps` back-to-back launches."""
+        ms = ctypes.c_double()
+        check(lib().itsd_profile_op(self.h, x.data_ptr(), t.data_ptr(), x.shape[0], int(op_index), int(reps),
+                                    ctypes.byref(ms), stream_ptr(x.device)))
+        return ms.value
 
     def profile_ops(self, x: torch.Tensor, t: torch.Tensor, max_ops: int = 512):
         import numpy as np
