@@ -55,18 +55,28 @@ template <typename T>
 __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (&acc)[2][2], int wm, int wn, int rl,
                                           int hh) {
   if constexpr (sizeof(T) == 2) {
+    // fragment reads two k-steps ahead of their MFMAs (two buffers, order pinned: the
+    // scheduler otherwise reads each k-step right before its MFMAs behind an lgkmcnt(0))
+    bf16x8 fa[2][2], fb[2][2];
+    auto rd = [&](int kk, int buf) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[buf][i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[buf][j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
+    };
+    rd(0, 0);
+    rd(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 af[2], bfg[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfg[j] = *(const bf16x8*)(B + swz(wn * 64 + j * 32 + rl, 2 * kk + hh));
+      const int b = kk & 1;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
+      if (kk + 2 < 4) rd(kk + 2, b);
+      __builtin_amdgcn_sched_barrier(0);
     }
   } else {
     // k mapping for the f32 MFMA: step s, lane half h -> k = 16h + s (A and B alike).
@@ -1113,25 +1123,57 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
     const int h = hrow[j];
     *(u32x4*)(hbuf + h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4)) = y;
   };
+  // The tap's 4 k-steps with the fragment reads two k-steps ahead of their MFMAs (two fragment
+  // buffers): left to itself the compiler reads each k-step right before its MFMAs and drains
+  // lgkmcnt(0) in front of every MFMA pair, exposing the LDS latency 8 times per tap.
   auto mma_tap = [&](const char* hbuf, int s, int tap) {
     if (a.dbg & 2) return;
     const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
     const char* A = wring + (s % NS) * TILEB;
+    const char* ar[2];
+    const char* br[2];
+    int bsw[2];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 af[2], bfg[2];
+    for (int i = 0; i < 2; ++i) ar[i] = A + (wm * 64 + i * 32 + rl) * ROWB;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(A + swz(wm * 64 + i * 32 + rl, 2 * kk + hh));
+    for (int j = 0; j < 2; ++j) {
+      const int h = hb[j] + toff;
+      br[j] = hbuf + h * ROWB;
+      bsw[j] = (h >> 1) & 7;
+    }
+    const int asw = (rl >> 1) & 7;  // rows wm*64 + i*32 + rl: (row >> 1) & 7 == (rl >> 1) & 7
+    bf16x8 fa[2][2], fb[2][2];
+    auto rd = [&](int kk, int buf) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int h = hb[j] + toff;
-        bfg[j] = *(const bf16x8*)(hbuf + h * ROWB + (((2 * kk + hh) ^ ((h >> 1) & 7)) << 4));
+      for (int i = 0; i < 2; ++i) fa[buf][i] = *(const bf16x8*)(ar[i] + (((2 * kk + hh) ^ asw) << 4));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[buf][j] = *(const bf16x8*)(br[j] + (((2 * kk + hh) ^ bsw[j]) << 4));
+    };
+    if constexpr (NSEG == 1) {
+      rd(0, 0);
+      rd(1, 1);
+      __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the reads back to their MFMAs)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int b = kk & 1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
+        if (kk + 2 < 4) rd(kk + 2, b);
+        __builtin_amdgcn_sched_barrier(0);
       }
+    } else {  // NSEG = 4 holds 7 halo items: no registers for the second fragment buffer
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int kk = 0; kk < 4; ++kk) {
+        rd(kk, 0);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      }
     }
   };
 
