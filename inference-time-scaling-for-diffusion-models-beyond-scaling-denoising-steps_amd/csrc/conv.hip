@@ -985,6 +985,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
 // one block owns the CU's 160 KiB of LDS, so the ring keeps more stages in flight. Per output,
 // the MFMA sequence (tap, channel chunk, k) and the epilogue are the 128-pixel kernels', so
 // without a K split the results are bit-identical to theirs.
+#ifdef ITSD_STAMPS
+// Diagnostic build only (hipcc -DITSD_STAMPS): per-wave cycle shares of the wide fused conv's
+// phases, [block % 1024][wave][phase] (the last launch to touch a slot wins). Never shipped.
+__device__ unsigned long long g_stamps[1024 * 8 * 8];
+__device__ __forceinline__ unsigned long long stamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP(var) const unsigned long long var = stamp()
+#define STAMP_ADD(slot, d) st[slot] += (d)
+#else
+#define STAMP(var)
+#define STAMP_ADD(slot, d)
+#endif
 constexpr int GNW_BN = 256;                                                   // pixels per tile
 constexpr int GNW_EPI = GNW_BN * EROW * 4 + (GNW_BN / 16) * 2 * CONV_BM * 4;  // E tile + statistics groups
 constexpr int GNW_SMEM = 160 * 1024;
@@ -1192,11 +1208,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
   // a third of the items each; taps 1-5 are a runtime loop (a fully unrolled chunk spills).
   constexpr int TW = 6;
   static_assert(TW >= NS, "the chunk's loads are retired before the first item write");
+#ifdef ITSD_STAMPS
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wait, barrier, issue, mma, transform, prologue, epilogue, total
+  const unsigned long long t_begin = stamp();
+#endif
   auto step = [&](int s0, int tap, const char* hcur, bool lpc_in_flight) {
+    STAMP(t0);
     if (lpc_in_flight) wait_vmcnt<2 * (NS - 2) + LPC>();
     else wait_vmcnt<2 * (NS - 2)>();
+    STAMP(t1);
     __builtin_amdgcn_s_barrier();
+    STAMP(t2);
     issue_w(s0 + tap + NS - 1);
+    STAMP(t3);
+    STAMP_ADD(0, t1 - t0);
+    STAMP_ADD(1, t2 - t1);
+    STAMP_ADD(2, t3 - t2);
+  };
+  auto mma_timed = [&](const char* hbuf, int s, int tap) {
+    STAMP(m0);
+    mma_tap(hbuf, s, tap);
+    STAMP(m1);
+    STAMP_ADD(3, m1 - m0);
   };
   auto run_chunk = [&](int cc, auto stage) {
     constexpr bool ST = decltype(stage)::value;
@@ -1209,31 +1242,49 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
       load_chunk(cc + 1);
       asm volatile("" ::: "memory");
     }
-    mma_tap(hcur, s0, 0);
+    mma_timed(hcur, s0, 0);
 #pragma unroll 1
     for (int tap = 1; tap < TW; ++tap) {
       step(s0, tap, hcur, ST && tap <= NS - 1);
-      mma_tap(hcur, s0 + tap, tap);
+      mma_timed(hcur, s0 + tap, tap);
     }
 #pragma unroll
     for (int k = 0; k < 9 - TW; ++k) {
       step(s0, TW + k, hcur, false);
-      mma_tap(hcur, s0 + TW + k, TW + k);
+      mma_timed(hcur, s0 + TW + k, TW + k);
       if constexpr (ST) {
+        STAMP(w0);
 #pragma unroll
         for (int j = k * ITEMS / 3; j < (k + 1) * ITEMS / 3; ++j) write_item(hnext, j);
+        STAMP(w1);
+        STAMP_ADD(4, w1 - w0);
       }
     }
     if constexpr (ST) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
+#ifdef ITSD_STAMPS
+  st[5] = stamp() - t_begin;  // prologue (first chunk staged)
+#endif
   for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
   run_chunk(ncc - 1, std::false_type{});
   wait_vmcnt<0>();
   __syncthreads();
   if (a.dbg & 16) return;
+  STAMP(e0);
   acc_to_E_wide(acc, (float*)smem);
   __syncthreads();
   epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
+#ifdef ITSD_STAMPS
+  __syncthreads();
+  const unsigned long long e1 = stamp();
+  st[6] = e1 - e0;
+  st[7] = e1 - t_begin;
+  if (lane == 0) {
+    const int b = (blockIdx.x + gridDim.x * blockIdx.y) & 1023;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g_stamps[(b * 8 + wid) * 8 + q] = st[q];
+  }
+#endif
 }
 
 // Plain implicit-GEMM conv (conv_pipe's work: 3x3 stride 2, the 4x4 level's 3x3s, 1x1s) at
@@ -1633,3 +1684,11 @@ template hipError_t launch_conv<float>(const ConvArgs&, hipStream_t);
 template hipError_t launch_conv<bf16_t>(const ConvArgs&, hipStream_t);
 
 }  // namespace itsd
+
+#ifdef ITSD_STAMPS
+// diagnostic builds only: copy the wide fused conv's per-wave phase cycles out
+extern "C" int itsd_debug_stamps(unsigned long long* host) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(itsd::g_stamps), sizeof(unsigned long long) * 1024 * 64) == hipSuccess ? 0 : 1;
+}
+#endif
