@@ -879,9 +879,10 @@ int itsd_set_option(const char* key, int value) {
     // in-loop loads (zero-page sources), 2 no MFMA, 8 no GN transform, 16 no epilogue,
     // 32 no epilogue output stores, 64 fused-conv halo loads from the zero page, 128 no
     // GN statistics pass, 256 no residual loads, 512 (wide fused
-    // conv) s_setprio 1 for waves 4-7 (results unchanged). (Never skip an issued load's wait: an
+    // conv) s_setprio 1 for waves 4-7 (results unchanged), 1024 / 2048 (wide
+    // fused conv) every lane reads the same B / A fragment row (LDS broadcast). (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
-    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512);
+    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048);
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {

@@ -1150,10 +1150,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
     const char* br[2];
     int bsw[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ar[i] = A + (wm * 64 + i * 32 + rl) * ROWB;
+    for (int i = 0; i < 2; ++i) ar[i] = A + ((a.dbg & 2048) ? 0 : (wm * 64 + i * 32 + rl) * ROWB);  // 2048: broadcast A reads
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int h = hb[j] + toff;
+      const int h = (a.dbg & 1024) ? 0 : hb[j] + toff;  // 1024: broadcast B reads (measurement only)
       br[j] = hbuf + h * ROWB;
       bsw[j] = (h >> 1) & 7;
     }

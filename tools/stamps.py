@@ -31,7 +31,7 @@ names = ["wait", "barrier", "issue", "mma", "transform", "prologue", "epilogue",
 sel = [int(v) for v in sys.argv[2:]] or [i for i, o in enumerate(ops) if o["kind"] in ("convgnw", "convgnw4")][:6]
 for i in sel:
     o = ops[i]
-    L.itsd_set_option(b"conv_dbg", 0)
+    L.itsd_set_option(b"conv_dbg", int(os.environ.get("ITSD_DBG", "0")))
     ms = nat.profile_op(x, t, i, reps=3)
     buf = np.zeros(1024 * 64, dtype=np.uint64)
     assert L.itsd_debug_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))) == 0
