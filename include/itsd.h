@@ -19,8 +19,9 @@
  *                                   223-248, 262-287), batched per candidate
  *   itsd_attention               <- AttnBlock core softmax(q k^T C^-0.5) v
  *                                   (Diffusion/Model.py:152-161, ModelCondition.py:105-115)
- *   itsd_profile_forward         <- (no reference counterpart) per-kernel census used
- *                                   by bench.py for the roofline line
+ *   itsd_profile_forward / _ops / _op, itsd_unet_query, itsd_set_option
+ *                                <- (no reference counterpart) per-kernel census used by
+ *                                   bench.py for the roofline line, introspection, A/B switches
  *
  * Conventions
  *  - Every tensor argument is a DEVICE pointer owned by the caller; the library
@@ -99,7 +100,9 @@ int itsd_set_schedule(itsd_unet* u, int T, const float* coeff1, const float* coe
                       const float* sqrt_var, float w);
 
 /* Run steps t_begin..t_end (inclusive, descending) of the ancestral sampler in
- * place on x[n,3,H,W]. noise == NULL: z ~ N(0,1) from counter-based Philox keyed
+ * place on x[n,3,H,W]. With ITSD_RUN_GRAPH one denoising step is captured per
+ * (n, x, labels, noise, option state) and replayed: seed, noise_offset and the clip
+ * step are device-side run parameters, so rounds that differ only in them reuse it. noise == NULL: z ~ N(0,1) from counter-based Philox keyed
  * (seed, step, noise_offset + element); otherwise noise is [T][n][3][H][W] fp32 and
  * step t uses noise[t] (t >= 1; the reference draws no noise at t = 0). labels: CFG only. */
 int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t_begin, int t_end,
@@ -150,6 +153,11 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
  * tile choices ("conv_variant", "splitk", "small_conv", "gn_wide", "conv_wide", "fuse_gn",
  * "io_mfma") and measurement-only ablations ("conv_dbg"). */
 int itsd_set_option(const char* key, int value);
+
+/* Introspection of a handle (no device work): "graph_captures" (step graphs captured and
+ * instantiated so far; a search replays one graph across all its rounds), "max_batch",
+ * "T_sched", "ws_bytes" (activation arena), "ops" (program length). */
+int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value);
 
 const char* itsd_last_error(void);
 int itsd_version(void);

@@ -34,6 +34,8 @@ hipError_t launch_linear(const float*, int, int, const float*, const float*, int
 hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hipStream_t);
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
+hipError_t launch_run_begin(int*, int, int*, RunParams*, const RunParams&, hipStream_t);
+int g_option_gen = 0;  // bumped by every itsd_set_option: part of the step-graph cache key
 bool conv_gn_eligible(int H, int W);
 int conv_gn_wide_segs(int H, int W, int M, int Cout);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
@@ -118,8 +120,12 @@ struct Arena {
   }
 };
 
+// A captured denoising step is keyed by what its launches bake in: the batch, whether labels
+// are used, the injected-noise pointer and the kernel-selection options. x and labels are
+// staged through handle-owned buffers and the seed, noise offset and clip step live in device
+// memory (RunParams), so every round of a search replays one graph.
 struct GraphEntry {
-  std::tuple<int, const float*, const int32_t*, const float*, unsigned long long, int, long long> key;
+  std::tuple<int, bool, const float*, int> key;
   hipGraphExec_t exec = nullptr;
 };
 
@@ -164,6 +170,10 @@ struct itsd_unet {
   float guide_w = 0.f, guide_w1 = 1.f;
   int* d_t = nullptr;
   int* d_nan = nullptr;
+  RunParams* d_run = nullptr;
+  float* x_state = nullptr;     // [max_batch][3][H][W]: the sampler's x between the caller's copies
+  int32_t* lab_state = nullptr; // [max_batch] labels of the guided sampler
+  long long graph_captures = 0;  // step graphs captured + instantiated (itsd_unet_query)
   void* zero_page = nullptr;  // 256 KiB of zeros (conv DMA source for padding, conv.hip zero_of_block)
   float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
   static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
@@ -856,6 +866,7 @@ int itsd_version(void) { return 1; }
 
 int itsd_set_option(const char* key, int value) {
   if (!key) return fail(ITSD_ERR_INVALID, "null key");
+  ++itsd::g_option_gen;  // cached step graphs baked in the previous kernel choices
   if (!std::strcmp(key, "conv_variant")) {
     if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "conv_variant in [0,3]");
     itsd::g_conv_variant = value;
@@ -900,6 +911,17 @@ int itsd_set_option(const char* key, int value) {
 
 const char* itsd_last_error(void) { return g_err.c_str(); }
 
+int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value) {
+  if (!u || !key || !value) return fail(ITSD_ERR_INVALID, "null argument");
+  if (!std::strcmp(key, "graph_captures")) *value = u->graph_captures;
+  else if (!std::strcmp(key, "max_batch")) *value = u->d.max_batch;
+  else if (!std::strcmp(key, "T_sched")) *value = u->T_sched;
+  else if (!std::strcmp(key, "ws_bytes")) *value = (int64_t)u->ws_bytes;
+  else if (!std::strcmp(key, "ops")) *value = (int64_t)u->ops.size();
+  else return fail(ITSD_ERR_INVALID, std::string("unknown query key ") + key);
+  return ITSD_OK;
+}
+
 int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights, int n_weights, int device,
                      itsd_unet** out) {
   if (!desc || !out || (!weights && n_weights)) return fail(ITSD_ERR_INVALID, "null argument");
@@ -926,6 +948,10 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipEventCreateWithFlags(&u->ev_out, hipEventDisableTiming));
   HIPCHK(hipMalloc(&u->d_t, 64));
   HIPCHK(hipMalloc(&u->d_nan, 64));
+  HIPCHK(hipMalloc(&u->d_run, sizeof(RunParams)));
+  HIPCHK(hipMemset(u->d_run, 0, sizeof(RunParams)));
+  HIPCHK(hipMalloc(&u->x_state, (size_t)d.max_batch * 3 * d.img_size * d.img_size * 4));
+  HIPCHK(hipMalloc(&u->lab_state, (size_t)d.max_batch * 4));
   HIPCHK(hipMalloc(&u->zero_page, 64 * 4096 + 1024));
   HIPCHK(hipMemset(u->zero_page, 0, 64 * 4096 + 1024));
   HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
@@ -946,7 +972,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   clear_graphs(u);
   hipFree(u->wdev); hipFree(u->ws); hipFree(u->emb_buf); hipFree(u->h1_buf); hipFree(u->te_buf);
   hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
-  hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->zero_page);
+  hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->d_run); hipFree(u->x_state); hipFree(u->lab_state); hipFree(u->zero_page);
   hipFree(u->splitk_ws);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
@@ -1013,23 +1039,29 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
   HIPCHK(hipEventRecord(u->ev_in, cs));
   HIPCHK(hipStreamWaitEvent(s, u->ev_in, 0));
   const int clip_at = (flags & ITSD_RUN_CLIP) ? t_end : -1;
+  const size_t xbytes = (size_t)n * 3 * u->H * u->H * 4;
+  HIPCHK(hipMemcpyAsync(u->x_state, x, xbytes, hipMemcpyDeviceToDevice, s));
+  if (labels) HIPCHK(hipMemcpyAsync(u->lab_state, labels, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+  float* xs = u->x_state;
+  const int32_t* ls = labels ? u->lab_state : nullptr;
 
   RunCtx c{};
   c.nb = u->cfg ? 2 * n : n;
-  c.x = x; c.x_mod = n;
+  c.x = xs; c.x_mod = n;
   c.temb = u->temb_table; c.tsel = u->d_t; c.temb_img_stride = 0;
-  c.labels = labels; c.label_mod = n; c.uncond_from = u->cfg ? n : -1;
+  c.labels = ls; c.label_mod = n; c.uncond_from = u->cfg ? n : -1;
   TailArgs& t = c.tail;
   t.n = n; t.cfg = u->cfg ? 1 : 0; t.guide_w = u->guide_w; t.guide_w1 = u->guide_w1;
-  t.step_mode = 1; t.x = x; t.tsel = u->d_t;
+  t.step_mode = 1; t.x = xs; t.tsel = u->d_t;
   t.coeff1 = u->coeff1; t.coeff2 = u->coeff2; t.sqrt_var = u->sqrt_var;
-  t.noise = noise; t.seed = seed; t.noise_offset = noise_offset; t.clip_at = clip_at; t.nan_flag = u->d_nan;
+  t.noise = noise; t.run = u->d_run; t.nan_flag = u->d_nan;
 
-  HIPCHK(hipMemsetAsync(u->d_nan, 0, 4, s));
-  HIPCHK(launch_set_int(u->d_t, t_begin, s));
+  RunParams rp{};
+  rp.seed = seed; rp.noise_offset = noise_offset; rp.clip_at = clip_at;
+  HIPCHK(launch_run_begin(u->d_t, t_begin, u->d_nan, u->d_run, rp, s));
   const int steps = t_begin - t_end + 1;
   if (flags & ITSD_RUN_GRAPH) {
-    auto key = std::make_tuple(n, (const float*)x, labels, noise, (unsigned long long)seed, clip_at, (long long)noise_offset);
+    auto key = std::make_tuple(n, labels != nullptr, noise, itsd::g_option_gen);
     hipGraphExec_t exec = nullptr;
     for (auto& g : u->graphs)
       if (g.key == key) exec = g.exec;
@@ -1046,6 +1078,7 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
       if (e != hipSuccess) return fail(ITSD_ERR_HIP, std::string("instantiate: ") + hipGetErrorString(e));
       if (u->graphs.size() >= 4) { hipGraphExecDestroy(u->graphs.front().exec); u->graphs.erase(u->graphs.begin()); }
       u->graphs.push_back({key, exec});
+      ++u->graph_captures;
     }
     for (int i = 0; i < steps; ++i) HIPCHK(hipGraphLaunch(exec, s));
   } else {
@@ -1054,6 +1087,7 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
       HIPCHK(launch_add_int(u->d_t, -1, s));
     }
   }
+  HIPCHK(hipMemcpyAsync(x, u->x_state, xbytes, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipEventRecord(u->ev_out, s));
   HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
   if (flags & ITSD_RUN_SYNC) {

@@ -131,6 +131,15 @@ struct HeadArgs {
   const bf16_t* wmf;    // bf16 MFMA weights [Cout][32] (k = ci*9 + tap, zero-padded 27..31), or null
 };
 
+// Per-run sampler parameters, kept in device memory so that one captured step graph serves
+// every run of a search (only the values change between rounds, never the graph).
+struct RunParams {
+  unsigned long long seed;  // Philox key of the per-step noise z
+  long long noise_offset;   // Philox element offset (global candidate index * per-candidate elements)
+  int clip_at;              // clip when t == clip_at (-1: never)
+  int pad_;
+};
+
 struct TailArgs {
   const void* g;        // NHWC [nb][H][W][C] : silu(gn(h))
   const float* w;       // [3][C][3][3] fp32 (reference layout)
@@ -146,9 +155,7 @@ struct TailArgs {
   const int* tsel;      // current step t (device)
   const float* coeff1; const float* coeff2; const float* sqrt_var;
   const float* noise;   // [T][n][3][H][W] or null
-  unsigned long long seed;
-  long long noise_offset;  // Philox element offset (global candidate index * per-candidate elements)
-  int clip_at;          // clip when t == clip_at (-1: never)
+  const RunParams* run; // seed / noise offset / clip step of this run (device)
   int* nan_flag;
   // bf16 MFMA tail (tail_mfma_kernel): g is the RAW last ResBlock output and the tail
   // GroupNorm+SiLU is applied while staging it, with per-image coefficients

@@ -602,11 +602,11 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs a) {
       const float mean = c1 * xv - c2 * eps[c];
       float xn = mean;
       if (t > 0) {
-        const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o] : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+        const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o] : philox_normal(a.run->seed, (unsigned)t, (unsigned long long)(a.run->noise_offset + (long long)o));
         xn = mean + sv * z;
       }
       bad |= (xn != xn);
-      if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+      if (t == a.run->clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
       a.x[o] = xn;
     }
     if (bad) atomicOr(a.nan_flag, 1);
@@ -709,11 +709,11 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
     float xn = mean;
     if (t > 0) {
       const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o]
-                              : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+                              : philox_normal(a.run->seed, (unsigned)t, (unsigned long long)(a.run->noise_offset + (long long)o));
       xn = mean + a.sqrt_var[t] * z;
     }
     if (xn != xn) atomicOr(a.nan_flag, 1);
-    if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+    if (t == a.run->clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
     a.x[o] = xn;
   }
 }
@@ -833,11 +833,11 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
       float xn = mean;
       if (t > 0) {
         const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o]
-                                : philox_normal(a.seed, (unsigned)t, (unsigned long long)(a.noise_offset + (long long)o));
+                                : philox_normal(a.run->seed, (unsigned)t, (unsigned long long)(a.run->noise_offset + (long long)o));
         xn = mean + a.sqrt_var[t] * z;
       }
       if (xn != xn) atomicOr(a.nan_flag, 1);
-      if (t == a.clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+      if (t == a.run->clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
       a.x[o] = xn;
     }
   }
@@ -1058,6 +1058,17 @@ hipError_t launch_noise(float* out, const float* pivot, int n_cand, long long pe
 
 // ============================================================================ small utilities
 __global__ void set_int_kernel(int* p, int v) { *p = v; }
+// start of a sampler run: step counter, NaN flag and the run's parameters (one launch, outside
+// the replayed step graph)
+__global__ void run_begin_kernel(int* t, int t_begin, int* nan_flag, RunParams* run, RunParams v) {
+  *t = t_begin;
+  *nan_flag = 0;
+  *run = v;
+}
+hipError_t launch_run_begin(int* t, int t_begin, int* nan_flag, RunParams* run, const RunParams& v, hipStream_t s) {
+  hipLaunchKernelGGL(run_begin_kernel, dim3(1), dim3(1), 0, s, t, t_begin, nan_flag, run, v);
+  return hipGetLastError();
+}
 __global__ void add_int_kernel(int* p, int v) { *p += v; }
 hipError_t launch_set_int(int* p, int v, hipStream_t s) {
   hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);

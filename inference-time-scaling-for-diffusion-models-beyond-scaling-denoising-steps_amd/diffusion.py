@@ -105,6 +105,25 @@ class GaussianDiffusionSampler:
 
     __call__ = forward
 
+    def reference_noise(self, shape: Sequence[int]) -> torch.Tensor:
+        """The T-1 draws one reference sampler call takes from the global CPU generator
+        (``Diffusion.py:94-96``: ``randn_like`` at t = T-1 .. 1), as [T, *shape] by step t."""
+        z = [torch.randn(tuple(shape)) for _ in range(self.T - 1)]
+        return torch.stack(z + [torch.zeros(tuple(shape))]).flip(0)
+
+    def denoise_fn(self, reference_rng: bool = True, labels: Optional[torch.Tensor] = None):
+        """A ``denoise_fn(noise, show_progress, **kw)`` for the sequential search API
+        (``search_algorithm.py:71``). reference_rng: each call consumes the reference's
+        per-step draws from the global generator (bit-identical candidates to the reference
+        loop under ``torch.manual_seed``); otherwise Philox seeded from that generator."""
+
+        def fn(noise: torch.Tensor, show_progress: bool = False, **kw) -> torch.Tensor:
+            z = self.reference_noise(noise.shape) if reference_rng else None
+            x = noise.to(self.model.device, torch.float32).clone().contiguous()
+            return self.run(x, labels=labels, noise=z)
+
+        return fn
+
 
 class CondGaussianDiffusionSampler(GaussianDiffusionSampler):
     """``DiffusionCondition.py:56``: guided eps = (1+w) eps(x,t,y) - w eps(x,t,0)."""
@@ -118,6 +137,11 @@ class CondGaussianDiffusionSampler(GaussianDiffusionSampler):
         return self.run(x, labels=labels, seed=seed, noise=noise, graph=graph)
 
     __call__ = forward
+
+    def denoise_fn(self, reference_rng: bool = True, labels: Optional[torch.Tensor] = None):
+        if labels is None:
+            raise ValueError("the guided sampler's denoise_fn needs labels")
+        return super().denoise_fn(reference_rng, labels)
 
 
 def reference_noise_plan(shape: Sequence[int], T: int, n_runs: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -226,12 +226,98 @@ def cfg_eval_labels(batch_size: int) -> torch.Tensor:
 
 
 def _device(cfg: Dict[str, Any]) -> torch.device:
-    dev = torch.device(cfg.get("device") or "cuda")
-    if dev.type != "cuda":
+    """``device`` (``Train.py:811``) and the inference config's ``device_ids`` /
+    ``use_multi_gpu`` (``abstract_metrics_from_pretrained_ddpm.py:52-123``). itsd runs one
+    process per GPU (torchrun) instead of DataParallel: under torchrun rank r takes
+    ``device_ids[LOCAL_RANK]`` (or ``cuda:LOCAL_RANK``); one process takes ``device_ids[0]``."""
+    spec = str(cfg.get("device") or "cuda")
+    if spec.split(":")[0] != "cuda":
         raise ValueError("itsd samples on the GPU only; set device: cuda")
+    ids = cfg.get("device_ids")
+    if isinstance(ids, str):
+        ids = [int(x) for x in ids.replace("[", "").replace("]", "").split(",") if x.strip()]
+    elif ids is not None and not isinstance(ids, (list, tuple)):
+        ids = [int(ids)]
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if ids:
+        if world > 1 and local >= len(ids):
+            raise ValueError(f"device_ids {list(ids)} has no entry for LOCAL_RANK {local}")
+        return torch.device("cuda", int(ids[local if world > 1 else 0]))
+    dev = torch.device(spec.split(",")[0])
     if dev.index is None:
-        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", torch.cuda.current_device())))
+        dev = torch.device("cuda", local if "LOCAL_RANK" in os.environ else torch.cuda.current_device())
     return dev
+
+
+def detect_checkpoint_T(state_dict: Dict[str, torch.Tensor]) -> Optional[int]:
+    """``abstract_metrics_from_pretrained_ddpm.py:163-188``: the row count of
+    ``time_embedding.timembedding.0.weight`` when it exceeds 500, else None.
+
+    For the functional DDPM embedding (``Model.py:38-42``) that tensor is the first Linear,
+    [4*ch, ch] = [512, 128] at ch = 128, so the reference "detects T = 512" there; for a
+    table embedding (``ModelCondition.py:38``, [T, ch]) it is the table's T."""
+    w = state_dict.get("time_embedding.timembedding.0.weight")
+    if w is not None and w.dim() == 2 and w.shape[0] > 500:
+        return int(w.shape[0])
+    return None
+
+
+def time_table(T: int, d_model: int, checkpoint_T: Optional[int] = None, strategy: str = "interpolate") -> torch.Tensor:
+    """The sinusoid table ``reinitialize_time_embedding`` builds
+    (``abstract_metrics_from_pretrained_ddpm.py:211-248``): sin/cos interleaved over
+    positions 0..T-1; with strategy "interpolate" and checkpoint_T < T the first
+    checkpoint_T rows are scaled by checkpoint_T / T."""
+    f = torch.exp(-(torch.arange(0, d_model, step=2) / d_model * math.log(10000)))
+    pos = torch.arange(T).float()
+    e = pos[:, None] * f[None, :]
+    e = torch.stack([torch.sin(e), torch.cos(e)], dim=-1).view(T, d_model)
+    if strategy == "interpolate" and checkpoint_T is not None and checkpoint_T < T:
+        out = e.clone()
+        out[:checkpoint_T] = e[:checkpoint_T] * (checkpoint_T / T)
+        return out
+    return e
+
+
+def adapt_time_embedding(state_dict: "OrderedDict[str, torch.Tensor]", net, cfg: Dict[str, Any]):
+    """T-mismatch handling of ``create_and_load_model`` (``abstract_metrics_from_pretrained_ddpm.py:
+    312-337``) for a checkpoint loaded into a model built with ``cfg["T"]``.
+
+    * functional DDPM embedding (itsd ``UNet``): T is not stored in any weight, so nothing is
+      replaced and every weight loads as trained. (The reference misreads the [512, 128] Linear
+      as a T = 512 table, drops every time_embedding weight and writes a [T, 128] sinusoid into
+      that Linear, whose forward then fails on the bias shape; itsd keeps the checkpoint.)
+    * table embedding (itsd ``CondUNet``, [T_ckpt, ch]): ``time_embedding_strategy``
+      "interpolate" / "reinit" rebuilds the table for T as the reference does and re-initialises
+      the embedding MLP (xavier-uniform weights, zero biases; ``:257-266``, seeded by
+      ``weight_seed``); "strict" (or no strategy key) raises.
+    Returns the (possibly rewritten) state dict."""
+    ck_T = detect_checkpoint_T(state_dict)
+    T = int(cfg["T"])
+    if ck_T is None or ck_T == T:
+        return state_dict
+    if not net.arch.cfg:
+        print(f"Functional time embedding: checkpoint tensor time_embedding.timembedding.0.weight "
+              f"{tuple(state_dict['time_embedding.timembedding.0.weight'].shape)} is the first MLP Linear, not a "
+              f"T={ck_T} table; T={T} needs no weight surgery (loading the checkpoint unchanged)")
+        return state_dict
+    strategy = (cfg.get("time_embedding_strategy") or "strict").lower()
+    if strategy not in ("interpolate", "reinit"):
+        raise ValueError(f"checkpoint time-embedding table has T={ck_T} rows, config T={T}; set "
+                         f"time_embedding_strategy: interpolate | reinit to rebuild it")
+    if cfg.get("fine_tune_time_embedding"):
+        print("fine_tune_time_embedding: ignored (itsd is inference-only)")
+    print(f"T mismatch: checkpoint T={ck_T}, config T={T}: rebuilding the time embedding ({strategy})")
+    sd = OrderedDict((k, v) for k, v in state_dict.items() if not k.startswith("time_embedding"))
+    d_model = int(state_dict["time_embedding.timembedding.0.weight"].shape[1])
+    sd["time_embedding.timembedding.0.weight"] = time_table(T, d_model, ck_T, strategy)
+    gen = torch.Generator().manual_seed(int(cfg.get("weight_seed") or 0))
+    for name in ("time_embedding.timembedding.1", "time_embedding.timembedding.3"):
+        w = torch.empty_like(state_dict[name + ".weight"])
+        torch.nn.init.xavier_uniform_(w, generator=gen)
+        sd[name + ".weight"] = w
+        sd[name + ".bias"] = torch.zeros_like(state_dict[name + ".bias"])
+    return sd
 
 
 def _weights(cfg: Dict[str, Any], net, dir_key: str) -> str:
@@ -241,7 +327,7 @@ def _weights(cfg: Dict[str, Any], net, dir_key: str) -> str:
         return "random"  # the facade already holds the seeded synthetic recipe
     if path is None:
         raise ValueError("weights: checkpoint needs test_load_weight (+ save_weight_dir/save_dir) or checkpoint_path")
-    net.load_state_dict(load_checkpoint_state_dict(path))
+    net.load_state_dict(adapt_time_embedding(load_checkpoint_state_dict(path), net, cfg))
     return path
 
 
@@ -271,6 +357,23 @@ def build_cfg_model(cfg: Dict[str, Any]):
     return net.eval()
 
 
+def _json_safe(v):
+    """NaN / +-inf scores as null (strict JSON)."""
+    if isinstance(v, float):
+        return v if math.isfinite(v) else None
+    if isinstance(v, dict):
+        return {k: _json_safe(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_json_safe(x) for x in v]
+    return v
+
+
+def _rank_world() -> Tuple[int, int]:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank(), torch.distributed.get_world_size()
+    return 0, 1
+
+
 def _search(cfg: Dict[str, Any], sampler, img_size: int, labels: Optional[torch.Tensor]) -> Optional[Dict[str, Any]]:
     s = cfg.get("search") or {}
     algo = (s.get("algorithm") or "none").lower()
@@ -279,17 +382,21 @@ def _search(cfg: Dict[str, Any], sampler, img_size: int, labels: Optional[torch.
     from .search import SearchEngine
     from .verifier import AestheticPredictor, OracleVerifier, SelfSupervisedVerifier
 
-    ver = {"oracle": OracleVerifier, "selfsup": SelfSupervisedVerifier,
-           "aesthetic": AestheticPredictor}[(s.get("verifier") or "oracle").lower()]()
-    eng = SearchEngine(sampler, ver, seed=int(cfg.get("seed") or 0))
+    vname = (s.get("verifier") or "oracle").lower()
+    ver = {"oracle": OracleVerifier, "selfsup": SelfSupervisedVerifier, "aesthetic": AestheticPredictor}[vname]()
     shape = (int(s.get("batch_per_candidate") or 1), 3, img_size, img_size)
+    if vname == "selfsup" and shape[0] < 2:
+        # verifier.py:243-246 averages the off-diagonal of the in-batch Gram matrix: one image
+        # per candidate has none, every score is NaN and the reference search never picks one
+        raise ValueError("search.verifier selfsup needs search.batch_per_candidate >= 2")
+    eng = SearchEngine(sampler, ver, seed=int(cfg.get("seed") or 0))
     lab = None if labels is None else labels[:shape[0]]
     if algo == "random":
         if lab is not None:
             raise ValueError("search.algorithm random is unconditional (search_algorithm.py:33-83)")
         best, score, hist = eng.random_search(int(s.get("n_candidates") or 4), shape)
     else:
-        init = torch.randn(shape, device=sampler.model.device)
+        init = eng.initial_noise(shape)  # the same pivot on every rank (Philox of the seed)
         if algo == "zero_order":
             best, score, hist = eng.zero_order_search(init, int(s.get("n_neighbors") or 4),
                                                       float(s.get("lambda_radius", 0.95)),
@@ -299,16 +406,46 @@ def _search(cfg: Dict[str, Any], sampler, img_size: int, labels: Optional[torch.
                                                 int(s.get("injection_step") or 400), labels=lab)
         else:
             raise ValueError(f"unknown search.algorithm '{algo}'")
-    x = best.clone()
-    sampler.run(x, labels=lab, seed=int(cfg.get("seed") or 0) + 7)
+    # the winner's own denoised image: kept by its owner rank during the search and broadcast
+    # once at the end -- the exact trajectory that earned best_score (not a re-run)
+    x = eng.best_image
     out = {"algorithm": algo, "best_score": score, "nfes": eng.nfes, "history": hist}
-    if eng.rank == 0:
-        d = cfg.get("sampled_dir") or "./SampledImgs/"
-        save_image(x * 0.5 + 0.5, os.path.join(d, s.get("bestImgName") or "SearchBestImgs.png"), nrow=cfg.get("nrow", 8))
-        with open(os.path.join(d, (s.get("bestImgName") or "SearchBestImgs.png").rsplit(".", 1)[0] + ".json"), "w") as fh:
-            json.dump(out, fh)
+    if eng.rank == 0 and x is not None:
+        d = _out_dir(cfg)
+        name = s.get("bestImgName") or "SearchBestImgs.png"
+        save_image(x * 0.5 + 0.5, os.path.join(d, name), nrow=cfg.get("nrow", 8))
+        with open(os.path.join(d, name.rsplit(".", 1)[0] + ".json"), "w") as fh:
+            json.dump(_json_safe(out), fh)
+    out["best_noise"] = best
     out["best_image"] = x
     return out
+
+
+def _out_dir(cfg: Dict[str, Any]) -> str:
+    """``sampled_dir`` (config.yaml) or ``sampled_images_save_dir`` (inference_config.yaml)."""
+    d = cfg.get("sampled_dir") or cfg.get("sampled_images_save_dir") or "./SampledImgs/"
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _sample_sharded(sampler, noisy: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``sampler(noisy[, labels])`` with the batch split over the ranks of a torchrun job:
+    every rank holds the same x_T draw (same seed), runs its contiguous slice with the
+    Philox noise of the slice's global image indices, and rank 0 gathers the result --
+    bit-identical to the single-process run. One process: a plain sampler call."""
+    rank, world = _rank_world()
+    if world == 1 or noisy.shape[0] % world:
+        return sampler(noisy) if labels is None else sampler(noisy, labels)
+    seed = torch.tensor([int(torch.randint(0, 2 ** 62, (1,)).item())], dtype=torch.int64, device=noisy.device)
+    torch.distributed.broadcast(seed, src=0)  # one sampler seed even if the ranks' generators differ
+    nl = noisy.shape[0] // world
+    per = noisy[0].numel()
+    x = noisy[rank * nl:(rank + 1) * nl].clone().contiguous()
+    lab = None if labels is None else labels[rank * nl:(rank + 1) * nl]
+    sampler.run(x, labels=lab, seed=int(seed.item()), noise_offset=rank * nl * per)
+    parts = [torch.empty_like(x) for _ in range(world)]
+    torch.distributed.all_gather(parts, x)
+    return torch.cat(parts)
 
 
 def eval(cfg: Dict[str, Any]) -> Dict[str, Any]:  # noqa: A001 (reference name)
@@ -328,11 +465,12 @@ def eval(cfg: Dict[str, Any]) -> Dict[str, Any]:  # noqa: A001 (reference name)
         sampler = GaussianDiffusionSampler(model, cfg["beta_1"], cfg["beta_T"], inference_T)
         img_size = int(cfg.get("img_size") or 256)
         noisy = torch.randn(size=[cfg["batch_size"], 3, img_size, img_size], device=model.device)
-        d = cfg["sampled_dir"]
-        os.makedirs(d, exist_ok=True)
-        save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]), nrow=cfg["nrow"])
-        imgs = sampler(noisy) * 0.5 + 0.5
-        save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
+        imgs = _sample_sharded(sampler, noisy) * 0.5 + 0.5
+        if _rank_world()[0] == 0:
+            d = _out_dir(cfg)
+            save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]),
+                       nrow=cfg["nrow"])
+            save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
         res = {"noisy": noisy, "sampled": imgs}
         res["search"] = _search(cfg, sampler, img_size, None)
     return res
@@ -352,13 +490,66 @@ def eval_condition(cfg: Dict[str, Any]) -> Dict[str, Any]:
         sampler = CondGaussianDiffusionSampler(model, cfg["beta_1"], cfg["beta_T"], cfg["T"], w=cfg["w"])
         img = int(cfg["img_size"])
         noisy = torch.randn(size=[cfg["batch_size"], 3, img, img], device=model.device)
-        d = cfg["sampled_dir"]
-        os.makedirs(d, exist_ok=True)
-        save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]), nrow=cfg["nrow"])
-        imgs = sampler(noisy, labels) * 0.5 + 0.5
-        save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
+        imgs = _sample_sharded(sampler, noisy, labels) * 0.5 + 0.5
+        if _rank_world()[0] == 0:
+            d = _out_dir(cfg)
+            save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]),
+                       nrow=cfg["nrow"])
+            save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
         res = {"noisy": noisy, "sampled": imgs, "labels": labels}
         res["search"] = _search(cfg, sampler, img, labels)
+    return res
+
+
+def image_filename(cfg: Dict[str, Any]) -> str:
+    """``generate_image_filename`` (``abstract_metrics_from_pretrained_ddpm.py:541-588``) without
+    metrics: <checkpoint dir name>_T<T>_bs<batch>_size<img>_<timestamp>."""
+    from datetime import datetime
+
+    ck = cfg.get("checkpoint_path") or ""
+    name = os.path.basename(os.path.dirname(ck)) if ck else "unknown"
+    name = name.replace("Checkpoints/", "").replace("checkpoints/", "") or "unknown"
+    parts = [name, f"T{cfg.get('T', 'unknown')}", f"bs{cfg.get('batch_size', 'unknown')}",
+             f"size{cfg.get('img_size', 'unknown')}", datetime.now().strftime("%Y%m%d_%H%M%S")]
+    return "_".join(str(p) for p in parts).replace("/", "-").replace("\\", "-").replace(":", "-")
+
+
+def infer(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    """Pretrained-checkpoint inference with the ``config/inference_config.yaml`` surface
+    (``abstract_metrics_from_pretrained_ddpm.py:649-694``): build the DDPM UNet with
+    ``T`` / ``channel`` / ... , load ``checkpoint_path`` with the T-mismatch handling of
+    ``adapt_time_embedding``, sample ``batch_size`` images at ``img_size`` with a T-step
+    sampler, and write ``sampled_images_save_dir/<generate_image_filename>.png`` and
+    ``output_dir/metrics_history.json`` (``save_results``, ``:604-646``).
+
+    The FID / IS / CLIP trajectory every ``metric_interval`` steps needs Inception / CLIP
+    weights that are downloaded at run time; they are unavailable offline, so
+    ``metric_history`` is empty and the JSON says why."""
+    from .diffusion import GaussianDiffusionSampler
+
+    if cfg.get("seed") is not None:
+        torch.manual_seed(int(cfg["seed"]))
+    with torch.no_grad():
+        model = build_ddpm(cfg)
+        sampler = GaussianDiffusionSampler(model, cfg["beta_1"], cfg["beta_T"], cfg["T"])
+        img = int(cfg.get("img_size") or 256)
+        x_T = torch.randn(size=[cfg["batch_size"], 3, img, img], device=model.device)
+        sampled = _sample_sharded(sampler, x_T)
+        res = {"noisy": x_T, "sampled": sampled * 0.5 + 0.5, "image_path": None}
+        if _rank_world()[0] == 0:
+            out_dir = cfg.get("output_dir") or "./inference_results"
+            os.makedirs(out_dir, exist_ok=True)
+            img_dir = cfg.get("sampled_images_save_dir") or os.path.join(out_dir, "sampled_images")
+            os.makedirs(img_dir, exist_ok=True)
+            path = os.path.join(img_dir, image_filename(cfg) + ".png")
+            save_image(res["sampled"], path, nrow=cfg.get("nrow", 8))
+            print(f"Sampled images saved to: {path}")
+            with open(os.path.join(out_dir, "metrics_history.json"), "w") as fh:
+                json.dump({"metric_history": [],
+                           "note": "FID/IS/CLIP need downloaded Inception/CLIP weights (unavailable offline)"},
+                          fh, indent=2)
+            res["image_path"] = path
+        res["search"] = _search(cfg, sampler, img, None)
     return res
 
 
@@ -374,7 +565,12 @@ def run(cfg: Dict[str, Any], condition: bool = False) -> Dict[str, Any]:
     if cfg.get("state", "eval") == "train":
         raise NotImplementedError("itsd is inference-only: training (Train.py:train) is out of scope; use state=eval")
     _maybe_init_dist(cfg)
-    return eval_condition(cfg) if condition else eval(cfg)
+    if condition:
+        return eval_condition(cfg)
+    # the inference_config.yaml surface has no sampled_dir / sampledImgName keys
+    if "sampledImgName" not in cfg and ("sampled_images_save_dir" in cfg or "output_dir" in cfg):
+        return infer(cfg)
+    return eval(cfg)
 
 
 def main(argv: Optional[Sequence[str]] = None, condition: bool = False, default_name: str = "config") -> Dict[str, Any]:

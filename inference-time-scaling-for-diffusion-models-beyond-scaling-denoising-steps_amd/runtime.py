@@ -68,6 +68,7 @@ _SIGS = {
                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
     "itsd_set_option": [ctypes.c_char_p, ctypes.c_int],
+    "itsd_unet_query": [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)],
     "itsd_last_error": [],
     "itsd_version": [],
 }
@@ -173,6 +174,12 @@ class NativeUNet:
         check(lib().itsd_sampler_run(self.h, x.data_ptr(), _ptr(labels), x.shape[0], int(t_begin), int(t_end),
                                      int(seed) & ((1 << 64) - 1), int(noise_offset), _ptr(noise), flags,
                                      stream_ptr(x.device)))
+
+    def query(self, key: str) -> int:
+        """itsd_unet_query: "graph_captures", "max_batch", "T_sched", "ws_bytes", "ops"."""
+        v = ctypes.c_int64()
+        check(lib().itsd_unet_query(self.h, key.encode(), ctypes.byref(v)))
+        return int(v.value)
 
     def profile_forward(self, x: torch.Tensor, t: torch.Tensor):
         cm, cf, tm = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()

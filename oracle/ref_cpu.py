@@ -269,3 +269,37 @@ def path_search(initial: Tensor, n_paths: int, injection_step: int, noise_scale:
         if s > best_score:
             best_score, best_noise = s, pert.clone()
     return best_noise, best_score, hist
+
+
+# --------------------------------------------------------------------------- counter-based noise
+def philox_normal(seed: int, step: int, idx) -> Tensor:
+    """The throughput mode's noise z(seed, step, element) -- NOT a reference function: the
+    reference draws ``torch.randn_like`` from the global generator (``Diffusion.py:96``), and
+    parity with it goes through injected noise. This restates itsd's own generator
+    (``csrc/kernels.hip`` philox_normal: Philox4x32-10, Salmon et al. SC'11, counter
+    (idx_lo, idx_hi, step, 0x1d5a1), key (seed_lo, seed_hi); Box-Muller on words 0, 1) in
+    numpy so that Philox-mode GPU runs can be checked step by step against this oracle."""
+    import numpy as np
+
+    M32 = np.uint64(0xFFFFFFFF)
+    idx = np.asarray(idx, dtype=np.uint64)
+    c0 = idx & M32
+    c1 = idx >> np.uint64(32)
+    c2 = np.full_like(c0, np.uint64(step & 0xFFFFFFFF))
+    c3 = np.full_like(c0, np.uint64(0x1D5A1))
+    k0 = np.uint64(seed & 0xFFFFFFFF)
+    k1 = np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & M32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & M32
+        n0 = hi1 ^ c1 ^ k0
+        n2 = hi0 ^ c3 ^ k1
+        c0, c1, c2, c3 = n0, lo1, n2, lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & M32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & M32
+    u1 = ((c0 >> np.uint64(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    u2 = (c1 >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    z = np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.float32(6.283185307179586) * u2)
+    return torch.from_numpy(z.astype(np.float32))

@@ -79,6 +79,25 @@ def test_archA64_eps():
     np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
 
 
+def test_archA256_eps():
+    """Arch A at the reference's ImageNet / inference_config resolution (256 px, attention S = 4096)."""
+    g = golden("archA256_eps")
+    a = dataclasses.replace(ARCH_A, img_size=256)
+    sd = synthetic_state_dict(a, 0)
+    with torch.no_grad():
+        eps = _fw(a, sd)(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]))
+    np.testing.assert_allclose(eps.numpy(), g["eps"], atol=FP32_EPS_TOL, rtol=0)
+
+
+def test_philox_restatement_statistics():
+    """oracle.philox_normal (itsd's counter-based generator restated in numpy): N(0,1)
+    moments over 2^18 draws and independence of the (step) counter word."""
+    z = R.philox_normal(7, 3, np.arange(1 << 18))
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1) < 0.01
+    z2 = R.philox_normal(7, 4, np.arange(1 << 18))
+    assert abs(torch.corrcoef(torch.stack([z, z2]))[0, 1].item()) < 0.01
+
+
 def _traj(a, sd, gname, bT, labels=None, w=0.0):
     g = golden(gname)
     T = int(g["T"])

@@ -109,6 +109,16 @@ def extra(M, MC, only):
             x = torch.randn(2, 3, 64, 64, generator=g)
             t = torch.tensor([3, 700])
             save("archA64_eps", x=x, t=t, eps=net(x, t))
+        if not only or "archA256_eps" in only:
+            # the reference's ImageNet resolution (example/imagenet_ep50_bs1024_T1000_lr1e-4.sh:30,
+            # config/inference_config.yaml img_size 256): attention at S = 4096, d = 384
+            a = dataclasses.replace(ARCH_A, img_size=256)
+            sd = synthetic_state_dict(a, seed=0)
+            net = ref_ddpm(M, a, sd)
+            g = torch.Generator().manual_seed(23)
+            x = torch.randn(1, 3, 256, 256, generator=g)
+            t = torch.tensor([400])
+            save("archA256_eps", x=x, t=t, eps=net(x, t))
 
 
 def main():
