@@ -100,6 +100,7 @@ struct Op {
   int ksize = 3, stride = 1, pad = 1, upsample = 0, zins = 0;
   int subpix = 0;  // upsample conv as 4 phase-wise 2x2 convs (conv.hip conv_pipe)
   size_t wt = 0, bias = 0;
+  size_t wfrag = SIZE_MAX;  // fragment-ordered copy of wt (fused GroupNorm convs, conv3x3_gn_reg_kernel)
   int Cout = 0, K = 0;
   int temb_col = -1;
   int resid = -1;
@@ -255,6 +256,23 @@ struct Builder {
     }
     return ar.add(tmp.data(), tmp.size() * 4);
   }
+  // [Cout][K] bf16 (k = (ky*ks+kx)*Cin + ci) -> MFMA A-fragment order [Cout/32][K/16][64][8]:
+  // lane L of k-step s holds W[32*cb + (L & 31)][16*s + 8*(L >> 5) + e] (v_mfma_f32_32x32x16_bf16).
+  size_t pack_frag(const float* Wsrc, int Cout, int Cin, int ks) {
+    const int K = ks * ks * Cin, nks = K / 16;
+    std::vector<uint16_t> b((size_t)Cout * K, 0);
+    if (Wsrc)
+      for (int cb = 0; cb < Cout / 32; ++cb)
+        for (int st = 0; st < nks; ++st)
+          for (int L = 0; L < 64; ++L)
+            for (int e = 0; e < 8; ++e) {
+              const int co = 32 * cb + (L & 31), k = 16 * st + 8 * (L >> 5) + e;
+              const int tap = k / Cin, ci = k - tap * Cin, ky = tap / ks, kx = tap - ky * ks;
+              b[(((size_t)cb * nks + st) * 64 + L) * 8 + e] =
+                  host_f2bf(Wsrc[(((size_t)co * Cin + ci) * ks + ky) * ks + kx]);
+            }
+    return ar.add(b.data(), b.size() * 2);
+  }
   // Nearest-x2 upsample + 3x3 conv (Model.py:123-125) as 4 sub-pixel phases: output
   // (2i+py, 2j+px) sees input rows i+dy+py-1 (dy in {0,1}) with the 3x3 taps folded
   // onto them: W'[ph][co][dy][dx][ci] = sum over ky in R(py,dy), kx in R(px,dx) of
@@ -353,6 +371,8 @@ struct Builder {
     int dst = act(Hout, Wout, Cout);
     conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
     u->ops.back().coef = coef;
+    if (coef != SIZE_MAX && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
+      u->ops.back().wfrag = pack_frag(W, Cout, Cin, ks);
     return dst;
   }
   // conv3x3(silu(GroupNorm(s1 ++ s2))) can run as one fused launch (conv3x3_gn_kernel)
@@ -666,6 +686,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.Hin = in.H; a.Win = in.W; a.Hout = out.H; a.Wout = out.W;
     a.ksize = o.ksize; a.stride = o.stride; a.pad = o.pad; a.upsample = o.upsample;
     a.wt = u->wdev + o.wt;
+    a.wfrag = o.wfrag != SIZE_MAX ? u->wdev + o.wfrag : nullptr;
     a.Cout = o.Cout; a.K = o.K;
     a.bias = u->wp(o.bias);
     if (o.temb_col >= 0) {
@@ -893,13 +914,19 @@ int itsd_set_option(const char* key, int value) {
     // conv) s_setprio 1 for waves 4-7 (results unchanged), 1024 / 2048 (wide
     // fused conv) every lane reads the same B / A fragment row (LDS broadcast). (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
-    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048);
+    // 4096 | (mask << 13): compile-time ablations of conv3x3_gn_reg_kernel<32> (conv.hip)
+    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13));
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {
     // 256-pixel conv tiles (conv3x3_gn_wide_kernel / conv_pipe_wide): 0 off, 1 auto, 2 whenever eligible
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, std::string(key) + " in [0,2]");
     (key[0] == 'g' ? itsd::g_gn_wide : itsd::g_conv_wide) = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "gn_reg")) {
+    if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "gn_reg in [0,3]");
+    itsd::g_gn_reg = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
@@ -935,6 +962,11 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
     if (d.attn[k] < 0 || d.attn[k] >= d.n_mult) return fail(ITSD_ERR_INVALID, "attn index out of bound");
   if (d.precision != ITSD_PREC_FP32 && d.precision != ITSD_PREC_BF16) return fail(ITSD_ERR_INVALID, "precision");
   HIPCHK(hipSetDevice(device));
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+      itsd::g_num_cus = cus;
+  }
   std::unique_ptr<itsd_unet> u(new itsd_unet());
   u->d = d;
   u->device = device;

@@ -11,6 +11,8 @@ extern int g_small_conv;   // 64x64-tile conv_small for small levels (itsd_set_o
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
 extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
+extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option "gn_reg")
+extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 
@@ -68,6 +70,8 @@ struct ConvArgs {
   int ksize, stride, pad, upsample;  // upsample: nearest x2 folded into addressing (Model.py:123)
   int zins;                          // zero-insertion (ConvTranspose2d s2 as a gather conv, ModelCondition.py:80)
   const void* wt;                    // packed [Cout][K], K = ksize*ksize*(C1+C2), k=(ky*ks+kx)*Cin+ci
+  const void* wfrag;                 // the same weights in MFMA A-fragment order [Cout/32][K/16][64][8]
+                                     // (fused GroupNorm convs, bf16), or null
   int Cout, K;
   const float* bias;                 // [Cout]
   // epilogue additive vectors (ResBlock temb_proj, Model.py:204; CFG cond_proj ModelCondition.py:156)

@@ -43,6 +43,10 @@ int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
+int g_gn_reg = 2;        // fused GroupNorm conv with the weights streamed into registers where the
+                         // 256-pixel tile applies: 0 off, 1 conv3x3_gn_reg_kernel, 2 warp-specialized
+                         // conv3x3_gn_ws_kernel (halo waves), 3 persistent conv3x3_gn_pws_kernel
+int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
                          // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
 
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
 #ifdef ITSD_STAMPS
 // Diagnostic build only (hipcc -DITSD_STAMPS): per-wave cycle shares of the wide fused conv's
 // phases, [block % 1024][wave][phase] (the last launch to touch a slot wins). Never shipped.
-__device__ unsigned long long g_stamps[1024 * 8 * 8];
+__device__ unsigned long long g_stamps[1024 * 16 * 8];  // [block % 1024][wave (<16)][slot]
 __device__ __forceinline__ unsigned long long stamp() {
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1282,9 +1286,672 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
   if (lane == 0) {
     const int b = (blockIdx.x + gridDim.x * blockIdx.y) & 1023;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) g_stamps[(b * 8 + wid) * 8 + q] = st[q];
+    for (int q = 0; q < 8; ++q) g_stamps[(b * 16 + wid) * 8 + q] = st[q];
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------- weights in registers
+// Fused GroupNorm+SiLU+conv3x3 with the A operand (weights) streamed straight into VGPRs.
+// The phase stamps of conv3x3_gn_wide_kernel put ~45 % of each tap outside the matrix pipe:
+// the per-tap s_barrier that retires a weight-ring slot (~430 cycles), the LDS-DMA issue of the
+// next slot (~290) and the halo transform (~250), all paid by both waves of a SIMD at the same
+// time. Here the weights never touch LDS:
+//   * weights are pre-packed in MFMA fragment order, wfrag[Cout/32][K/16][64 lanes][8 k]
+//     (bf16): one 16-B load per lane per k-step, 1 KiB per wave-instruction, fully coalesced;
+//   * wave w owns couts 32*(w&3) .. +31 (one A fragment per k-step) and pixels 128*(w>>2) .. +127
+//     (four B fragments from the LDS halo); waves w and w+4 share a SIMD and read the same
+//     weights (the second read is an L1 hit);
+//   * the A fragment of k-step s+5 is loaded while k-step s computes (a 6-slot register ring;
+//     36 k-steps per 64-channel chunk, so the slot of a k-step is static); the only block barrier
+//     is the one per chunk that publishes the next chunk's GroupNorm+SiLU'd halo
+//     (double-buffered; loaded in three item groups at taps 0/2/4 and transformed at taps 3/5/7,
+//     beside the other waves' MFMAs).
+// W (image width) is a template argument: the halo addressing divides by W + 2.
+// Per output the MFMA sequence (chunk, tap, k-step) and the epilogue are conv3x3_gn_wide_kernel's,
+// so the result is bit-identical to it.
+template <int W> struct GnrCfg;
+template <> struct GnrCfg<32> { static constexpr int NSEG = 1, ITEMS = 6; };  // 8 rows + border: 10 x 34
+template <> struct GnrCfg<16> { static constexpr int NSEG = 1, ITEMS = 6; };  // one image + border: 18 x 18
+template <> struct GnrCfg<8> { static constexpr int NSEG = 4, ITEMS = 7; };   // four images: 4 x 10 x 10
+constexpr int GNR_RING = 6;  // A k-step slots in flight (prefetch distance 5 k-steps)
+
+// AB: compile-time ablations for measurement builds only (conv_dbg 4096 + AB << 13; results wrong
+// when set): 1 no MFMA, 2 no A loads, 4 no B LDS reads, 8 no halo loads / transform, 16 no epilogue,
+// 32 no GroupNorm+SiLU arithmetic (raw halo copied), 64 no halo LDS writes.
+template <int W, int AB = 0>
+__global__ __launch_bounds__(512, 1) void conv3x3_gn_reg_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int NSEG = GnrCfg<W>::NSEG, ITEMS = GnrCfg<W>::ITEMS;
+  constexpr int W2 = W + 2;
+  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;  // output rows of one image segment (square images)
+  constexpr int HS = (THs + 2) * W2;              // halo rows of one segment
+  constexpr int HALO = ITEMS * 64 * ROWB;         // one halo buffer
+  constexpr int TPS = 512 / NSEG, RPP = TPS / 8;  // threads per image segment, its halo rows per pass
+  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
+  static_assert(2 * HALO <= GNW_SMEM, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar addressing
+  const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
+  const int H = a.Hout;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64;
+  const int img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
+  const T* zero = zero_of_block<T>(a);
+
+  int hb[4];  // halo row of this lane's pixel in B tile j at tap (0,0)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pl = wn * 128 + j * 32 + rl;
+    const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
+    hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+  }
+  const int kpt = Cin >> 4;  // k-steps per tap
+  // this wave's A fragments: scalar base + lane * 16 B (global_load saddr form, one VGPR offset)
+  const char* abase = (const char*)a.wfrag + (size_t)((tileC >> 5) + wm) * (9 * kpt) * 1024;
+  const int alane = lane * 16;
+  const int lch = tid & 7, sg = tid / TPS, lt = tid - sg * TPS;
+  // halo item j of this thread: row r = lt/8 + RPP*j of its segment; input pixel or -1 (padding /
+  // scratch rows past the segment, written but never read)
+  auto item_row = [&](int j) { return (lt >> 3) + RPP * j; };
+  auto item_pix = [&](int j) -> int {  // branch-free (selects, no exec-mask branches)
+    const int r = item_row(j);
+    const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    return ok ? ((img0 + sg) * H + iy) * W + ix : -1;
+  };
+  auto item_lds = [&](int j) {
+    const int r = item_row(j);
+    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
+    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  u32x4 ra[GNR_RING];   // A fragments of the k-steps in flight
+  u32x4 hreg[ITEMS];    // next chunk's raw halo items (a group at a time is live)
+  f32x4 cf[4];          // a[8], b[8] of this lane's 8 channels, its segment's image, next chunk
+  auto load_a = [&](int cc, int step, u32x4& dst) {  // step = tap * 4 + kk of chunk cc
+    const int tap = step >> 2, kk = step & 3;
+    if constexpr (AB & 2) dst = u32x4{(uint32_t)step, 0u, 0u, 0u};
+    else dst = *(const u32x4*)(abase + (size_t)(tap * kpt + cc * 4 + kk) * 1024 + alane);
+  };
+  auto load_items = [&](int cc, int j0, int j1) {
+    if constexpr ((AB & 8) != 0) return;
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int Cs = s1 ? a.C1 : a.C2;
+    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      const int po = item_pix(j);
+      hreg[j] = *(const u32x4*)(po >= 0 ? src + (unsigned)(po * Cs + cs0) : zero);
+    }
+  };
+  auto load_coef = [&](int cc) {
+    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cf[q] = cp[q];
+  };
+  // silu(x*a + b) in scalar f32 (packed f32 VALU beside MFMAs costs more than it saves,
+  // MI355X_MICROARCH.md 'price of one filler'); same operations as gn_silu2, so bit-identical
+  auto gn_silu1 = [](float x, float sc, float sh) {
+    const float y = x * sc + sh;
+    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
+  };
+  auto write_item = [&](char* hbuf, int j) {
+    if constexpr ((AB & 8) != 0) return;
+    const uint32_t* xw = (const uint32_t*)&hreg[j];
+    u32x4 y = hreg[j];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
+      if constexpr ((AB & 32) != 0) break;
+      const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
+      const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
+      const int e = 2 * (w & 1);
+      const float r0 = gn_silu1(x0, av[e], bv[e]), r1 = gn_silu1(x1, av[e + 1], bv[e + 1]);
+      y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+    }
+    const bool pad = item_pix(j) < 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
+    if constexpr ((AB & 64) != 0) {
+      if (y[0] == 0x12345u) *(u32x4*)(hbuf + item_lds(j)) = y;
+    } else {
+      *(u32x4*)(hbuf + item_lds(j)) = y;
+    }
+  };
+  auto block_sync = [&]() {  // this wave's LDS writes done, then the workgroup barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // item groups of the next chunk's halo: loaded at taps 0 / 2 / 4, transformed at 3 / 5 / 7
+  constexpr int G1 = ITEMS / 3, G2 = 2 * (ITEMS / 3);
+
+  // Epilogue inputs staged up front. LDS map: halos [0, 2*HALO) during the loop, then the fp32
+  // tile E [256][EROW] over them; behind E: addv = bias + temb (+ CFG cond) per (image of the
+  // tile, cout) and the statistics partials of the 8 waves.
+  constexpr int NIMT = NSEG;                     // images of the tile (W = 8: four)
+  float* addv = (float*)smem + GNW_BN * EROW;    // [NIMT][128]
+  float* spart = addv + NIMT * CONV_BM;          // [8 waves][2][128]
+  static_assert((GNW_BN * EROW + NIMT * CONV_BM + 8 * 2 * CONV_BM) * 4 <= GNW_SMEM, "epilogue LDS");
+  static_assert(2 * HALO <= GNW_BN * EROW * 4, "halos lie under E");
+  {
+    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+    for (int it = tid; it < NIMT * CONV_BM; it += 512) {
+      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
+      float v = a.bias[co];
+      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
+      if (a.cemb) {
+        int lab = 0;
+        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
+        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
+      }
+      addv[it] = v;
+    }
+  }
+  // epilogue thread map: 8 consecutive couts (ecq * 8) of 8 consecutive pixel rows (8 * erg ..),
+  // so a wave's rows (32 of them) lie in one GroupNorm statistics slot (>= 64 pixels)
+  const int ecq = tid & 15, erg = tid >> 4;
+  u32x4 rres[8];  // the residual rows, prefetched during the last chunk
+  auto load_resid = [&]() {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      rres[k] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + 8 * erg + k) * a.Cout + tileC + ecq * 8);
+  };
+
+  // prologue: chunk 0's halo and the first 5 k-steps' weights
+  load_coef(0);
+  load_items(0, 0, ITEMS);
+#pragma unroll
+  for (int st = 0; st < GNR_RING - 1; ++st) load_a(0, st, ra[st]);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) write_item(smem, j);
+  block_sync();
+
+  auto run_chunk = [&](int cc, auto stage) {
+    constexpr bool ST = decltype(stage)::value;
+    const char* hcur = smem + (cc & 1) * HALO;
+    char* hnext = smem + ((cc + 1) & 1) * HALO;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (ST && tap == 0) {
+        load_coef(cc + 1);
+        load_items(cc + 1, 0, G1);
+      }
+      if (ST && tap == 2) load_items(cc + 1, G1, G2);
+      if (ST && tap == 4) load_items(cc + 1, G2, ITEMS);
+      if (!ST && tap == 2 && a.resid) load_resid();
+      const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
+      // B addresses rebuilt per tap from an opaque copy of hb: left alone, the compiler hoists
+      // all 144 per-chunk addresses out of the chunk loop and spills them
+      int hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hv[j] = hb[j] + toff;
+        asm volatile("" : "+v"(hv[j]));
+      }
+      bf16x8 fb[2][4];
+      auto rd = [&](int kk, int buf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr ((AB & 4) != 0) fb[buf][j] = bf16x8{(short)hv[j], 0, 0, 0, 0, 0, 0, (short)kk};
+          else fb[buf][j] = *(const bf16x8*)(hcur + hv[j] * ROWB + (((2 * kk + hh) ^ ((hv[j] >> 1) & 7)) << 4));
+        }
+      };
+      rd(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int step = tap * 4 + kk;
+        // prefetch k-step step + 5 (past the chunk's end: the next chunk's first k-steps)
+        const int pf = step + GNR_RING - 1;
+        if (pf < 36) load_a(cc, pf, ra[pf % GNR_RING]);
+        else if (ST) load_a(cc + 1, pf - 36, ra[pf % GNR_RING]);
+        if (kk + 1 < 4) rd(kk + 1, (kk + 1) & 1);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr ((AB & 1) != 0) acc[j][0] += (float)af[0] + (float)fb[kk & 1][j][0];
+          else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[kk & 1][j], acc[j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ST && tap == 3) {
+#pragma unroll
+        for (int j = 0; j < G1; ++j) write_item(hnext, j);
+      }
+      if (ST && tap == 5) {
+#pragma unroll
+        for (int j = G1; j < G2; ++j) write_item(hnext, j);
+      }
+      if (ST && tap == 7) {
+#pragma unroll
+        for (int j = G2; j < ITEMS; ++j) write_item(hnext, j);
+      }
+    }
+    if (ST) block_sync();
+  };
+  for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
+  run_chunk(ncc - 1, std::false_type{});
+  block_sync();  // every wave is done reading the halos: the epilogue's E tile overlays them
+  float* E = (float*)smem;
+  if constexpr ((AB & 16) != 0) {  // keep the accumulators alive, skip the epilogue
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc[j][r];
+    if (s == 1.2345f) E[tid] = s;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v4 = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+      *(f32x4*)(E + (wn * 128 + j * 32 + rl) * EROW + wm * 32 + 8 * g + 4 * hh) = v4;
+    }
+  __syncthreads();
+  // + addv + residual, rounded once, 16-B stores; the consumer GroupNorm's per-channel (sum,
+  // sum of squares) of the rounded values accumulated in registers over the thread's 8 rows
+  const int HWo = H * W;
+  const float* av = addv + (NSEG == 1 ? 0 : (8 * erg) / HWo) * CONV_BM + ecq * 8;
+  float s8[8], q8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s8[e] = q8[e] = 0.f;
+  const f32x4 a0 = *(const f32x4*)av, a1 = *(const f32x4*)(av + 4);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int r = 8 * erg + k;
+    const f32x4 e0 = *(const f32x4*)(E + r * EROW + ecq * 8), e1 = *(const f32x4*)(E + r * EROW + ecq * 8 + 4);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = e0[e] + a0[e];
+      v[4 + e] = e1[e] + a1[e];
+    }
+    if (a.resid) {
+      const T* re = (const T*)&rres[k];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bf2f(re[e]);
+    }
+    u32x4 w;
+    T* we = (T*)&w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      we[e] = f2bf(v[e]);
+      const float rv = bf2f(we[e]);
+      s8[e] += rv;
+      q8[e] = fmaf(rv, rv, q8[e]);
+    }
+    *(u32x4*)((T*)a.out + (size_t)(tileP + r) * a.Cout + tileC + ecq * 8) = w;
+  }
+  if (!a.stats) return;
+  // lanes l, l+16, l+32, l+48 hold the same 8 channels: butterfly over them, then one row of
+  // partials per wave in LDS; slot sums in fixed wave order (deterministic, no atomics)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s8[e] += __shfl_xor(s8[e], 16, 64);
+    q8[e] += __shfl_xor(q8[e], 16, 64);
+    s8[e] += __shfl_xor(s8[e], 32, 64);
+    q8[e] += __shfl_xor(q8[e], 32, 64);
+  }
+  if (lane < 16) {
+    float* sp = spart + (size_t)wid * 2 * CONV_BM + ecq * 8;
+    *(f32x4*)sp = f32x4{s8[0], s8[1], s8[2], s8[3]};
+    *(f32x4*)(sp + 4) = f32x4{s8[4], s8[5], s8[6], s8[7]};
+    *(f32x4*)(sp + CONV_BM) = f32x4{q8[0], q8[1], q8[2], q8[3]};
+    *(f32x4*)(sp + CONV_BM + 4) = f32x4{q8[4], q8[5], q8[6], q8[7]};
+  }
+  __syncthreads();
+  constexpr int SLOT = (NSEG == 1 ? 128 : 64);  // stat_slot_px(HW): 128, or HW = 64 at 8x8
+  constexpr int WPS = SLOT / 32;                // waves per slot
+  for (int it = tid; it < (GNW_BN / SLOT) * CONV_BM; it += 512) {
+    const int sl = it / CONV_BM, cl = it % CONV_BM;
+    float sum = 0.f, sq = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) {
+      sum += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + cl];
+      sq += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + CONV_BM + cl];
+    }
+    const long long slot = (long long)tileP / SLOT + sl;
+    a.stats[(slot * 2) * a.Cout + tileC + cl] = sum;
+    a.stats[(slot * 2 + 1) * a.Cout + tileC + cl] = sq;
+  }
+}
+
+// ---------------------------------------------------------------------------- warp-specialized
+// conv3x3_gn_reg_kernel with the GroupNorm+SiLU halo work moved to dedicated waves. Ablations of
+// the register kernel put ~30 % of its time in the halo loads + transform (VALU that the MFMA
+// waves issued between their own MFMAs) and ~27 % in the epilogue. Here a 768-thread block runs
+//   * waves 0..7 (MFMA waves): exactly the register kernel's MFMA loop (A fragments streamed into
+//     VGPRs, B from the LDS halo, one barrier per 64-channel chunk) and nothing else;
+//   * waves 8..11 (one per SIMD, "halo waves"): load + GroupNorm+SiLU + LDS-write the next
+//     chunk's halo while the MFMA waves compute the current one (MFMA and VALU pipes run
+//     concurrently on a SIMD), prefetch the residual rows during the last chunk, and run the
+//     epilogue's output pass (+ bias/temb/residual, rounding, 16-B stores, GroupNorm statistics).
+// 3 waves per SIMD: 168 VGPRs each. The MFMA sequence per output equals the register kernel's.
+template <int W> struct GnsCfg;
+template <> struct GnsCfg<32> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 10 x 34 halo rows
+template <> struct GnsCfg<16> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 18 x 18
+template <> struct GnsCfg<8> { static constexpr int NSEG = 4, ITEMS = 13; };   // 4 x 104 >= 4 x 10 x 10
+
+template <int W>
+__global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int NSEG = GnsCfg<W>::NSEG, ITEMS = GnsCfg<W>::ITEMS;
+  constexpr int W2 = W + 2;
+  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;  // output rows of one image segment
+  constexpr int HS = (THs + 2) * W2;              // halo rows of one segment
+  constexpr int TPS = 256 / NSEG, RPP = TPS / 8;  // halo-wave threads per segment, rows per pass
+  constexpr int HROWS = NSEG * ITEMS * RPP;       // halo rows incl. scratch
+  constexpr int HALO = HROWS * ROWB;
+  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
+  static_assert(2 * HALO <= GNW_BN * EROW * 4, "halos lie under E");
+  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
+  float* const E = (float*)smem;
+  float* const addv = E + GNW_BN * EROW;        // [NSEG][128]
+  float* const spart = addv + NSEG * CONV_BM;   // [4 halo waves][2][128]
+  static_assert((GNW_BN * EROW + NSEG * CONV_BM + 4 * 2 * CONV_BM) * 4 <= GNW_SMEM, "epilogue LDS");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const TileId bt = tile_of_block();
+  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
+  const int H = a.Hout;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64;
+  const int img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
+#ifdef ITSD_STAMPS
+  // MFMA waves: 0 chunk compute, 1 barrier wait, 5 prologue, 6 epilogue, 7 total; halo waves:
+  // 3 halo staging, 1 barrier wait, 5 chunk-0 staging, 6 output pass
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_begin = stamp();
+  auto stamps_out = [&]() {
+    st[7] = stamp() - t_begin;
+    if (lane == 0) {
+      const int b = (blockIdx.x + gridDim.x * blockIdx.y) & 1023;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g_stamps[(b * 16 + wid) * 8 + q] = st[q];
+    }
+  };
+#define WS_STAMP_OUT() stamps_out()
+#else
+#define WS_STAMP_OUT()
+#endif
+  auto block_sync = [&]() {  // this wave's LDS writes done, then the workgroup barrier
+    STAMP(b0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    STAMP(b1);
+    STAMP_ADD(1, b1 - b0);
+  };
+  // addv = bias + temb (+ CFG cond) per (image of the tile, cout), behind E
+  {
+    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+    for (int it = tid; it < NSEG * CONV_BM; it += 768) {
+      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
+      float v = a.bias[co];
+      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
+      if (a.cemb) {
+        int lab = 0;
+        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
+        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
+      }
+      addv[it] = v;
+    }
+  }
+
+  if (wid < 8) {
+    // ================================================================ MFMA waves
+    const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
+    int hb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = wn * 128 + j * 32 + rl;
+      const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
+      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+    }
+    const int kpt = Cin >> 4;
+    const char* abase = (const char*)a.wfrag + (size_t)((tileC >> 5) + wm) * (9 * kpt) * 1024;
+    const int alane = lane * 16;
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    u32x4 ra[GNR_RING];
+    auto load_a = [&](int cc, int step, u32x4& dst) {
+      const int tap = step >> 2, kk = step & 3;
+      dst = *(const u32x4*)(abase + (size_t)(tap * kpt + cc * 4 + kk) * 1024 + alane);
+    };
+#pragma unroll
+    for (int s0 = 0; s0 < GNR_RING - 1; ++s0) load_a(0, s0, ra[s0]);
+#ifdef ITSD_STAMPS
+    st[5] = stamp() - t_begin;
+#endif
+    block_sync();  // B0: chunk 0's halo is in buffer 0
+    auto run_chunk = [&](int cc, auto stage) {
+      constexpr bool ST = decltype(stage)::value;
+      STAMP(c0);
+      const char* hcur = smem + (cc & 1) * HALO;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
+        int hv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hv[j] = hb[j] + toff;
+          asm volatile("" : "+v"(hv[j]));
+        }
+        bf16x8 fb[2][4];
+        auto rd = [&](int kk, int buf) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            fb[buf][j] = *(const bf16x8*)(hcur + hv[j] * ROWB + (((2 * kk + hh) ^ ((hv[j] >> 1) & 7)) << 4));
+        };
+        rd(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int step = tap * 4 + kk;
+          const int pf = step + GNR_RING - 1;
+          if (pf < 36) load_a(cc, pf, ra[pf % GNR_RING]);
+          else if (ST) load_a(cc + 1, pf - 36, ra[pf % GNR_RING]);
+          if (kk + 1 < 4) rd(kk + 1, (kk + 1) & 1);
+          const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[kk & 1][j], acc[j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      STAMP(c1);
+      STAMP_ADD(0, c1 - c0);
+      block_sync();  // chunk done (halo buffer free); next chunk's halo published
+    };
+    for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
+    run_chunk(ncc - 1, std::false_type{});
+    // the last barrier above ends every halo read: E overlays the halos
+    STAMP(e0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v4 = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+        *(f32x4*)(E + (wn * 128 + j * 32 + rl) * EROW + wm * 32 + 8 * g + 4 * hh) = v4;
+      }
+    block_sync();  // E1: the fp32 tile is complete
+    if (a.stats) block_sync();  // E2 (the halo waves' statistics partials)
+#ifdef ITSD_STAMPS
+    st[6] = stamp() - e0;
+#endif
+    WS_STAMP_OUT();
+    return;
+  }
+
+  // ================================================================== halo waves
+  const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
+  const T* zero = zero_of_block<T>(a);
+  auto item_row = [&](int j) { return (lt >> 3) + RPP * j; };
+  auto item_pix = [&](int j) -> int {
+    const int r = item_row(j);
+    const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    return ok ? ((img0 + sg) * H + iy) * W + ix : -1;
+  };
+  auto item_lds = [&](int j) {
+    const int r = item_row(j);
+    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
+    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
+  };
+  auto gn_silu1 = [](float x, float sc, float sh) {
+    const float y = x * sc + sh;
+    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
+  };
+  // one chunk's halo: all item loads in flight, then transform + LDS write item by item
+  auto stage_chunk = [&](int cc, char* hbuf) {
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int Cs = s1 ? a.C1 : a.C2;
+    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
+    u32x4 hreg[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int po = item_pix(j);
+      hreg[j] = *(const u32x4*)(po >= 0 ? src + (unsigned)(po * Cs + cs0) : zero);
+    }
+    f32x4 cf[4];
+    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cf[q] = cp[q];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t* xw = (const uint32_t*)&hreg[j];
+      u32x4 y;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
+        const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
+        const int e = 2 * (w & 1);
+        const float r0 = gn_silu1(x0, av[e], bv[e]), r1 = gn_silu1(x1, av[e + 1], bv[e + 1]);
+        y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+      }
+      const bool pad = item_pix(j) < 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
+      *(u32x4*)(hbuf + item_lds(j)) = y;
+    }
+  };
+  stage_chunk(0, smem);
+#ifdef ITSD_STAMPS
+  st[5] = stamp() - t_begin;
+#endif
+  block_sync();  // B0
+  for (int cc = 0; cc + 1 < ncc; ++cc) {
+    STAMP(h0);
+    stage_chunk(cc + 1, smem + ((cc + 1) & 1) * HALO);
+#ifdef ITSD_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    STAMP(h1);
+    STAMP_ADD(3, h1 - h0);
+    block_sync();  // end of MFMA chunk cc
+  }
+  // last chunk: prefetch the residual rows of this thread's epilogue share
+  const int ecq = tt & 15, erg = tt >> 4;  // 8 couts (ecq*8) of 16 rows (16*erg ..)
+  u32x4 rres[16];
+  if (a.resid) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      rres[k] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + 16 * erg + k) * a.Cout + tileC + ecq * 8);
+  }
+  block_sync();  // end of the last MFMA chunk
+  block_sync();  // E1
+  STAMP(o0);
+  // output pass: + addv + residual, rounded once, 16-B stores, the consumer GroupNorm's
+  // per-channel (sum, sum of squares) of the rounded values
+  const int HWo = H * W;
+  const float* av = addv + (NSEG == 1 ? 0 : (16 * erg) / HWo) * CONV_BM + ecq * 8;
+  const f32x4 a0 = *(const f32x4*)av, a1 = *(const f32x4*)(av + 4);
+  float s8[8], q8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s8[e] = q8[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = 16 * erg + k;
+    const f32x4 e0 = *(const f32x4*)(E + r * EROW + ecq * 8), e1 = *(const f32x4*)(E + r * EROW + ecq * 8 + 4);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = e0[e] + a0[e];
+      v[4 + e] = e1[e] + a1[e];
+    }
+    if (a.resid) {
+      const T* re = (const T*)&rres[k];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bf2f(re[e]);
+    }
+    u32x4 w;
+    T* we = (T*)&w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      we[e] = f2bf(v[e]);
+      const float rv = bf2f(we[e]);
+      s8[e] += rv;
+      q8[e] = fmaf(rv, rv, q8[e]);
+    }
+    *(u32x4*)((T*)a.out + (size_t)(tileP + r) * a.Cout + tileC + ecq * 8) = w;
+  }
+  if (!a.stats) {
+#ifdef ITSD_STAMPS
+    st[6] = stamp() - o0;
+#endif
+    WS_STAMP_OUT();
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s8[e] += __shfl_xor(s8[e], 16, 64);
+    q8[e] += __shfl_xor(q8[e], 16, 64);
+    s8[e] += __shfl_xor(s8[e], 32, 64);
+    q8[e] += __shfl_xor(q8[e], 32, 64);
+  }
+  const int hw = wid - 8;  // halo wave 0..3: rows 64*hw .. +63
+  if (lane < 16) {
+    float* sp = spart + (size_t)hw * 2 * CONV_BM + ecq * 8;
+    *(f32x4*)sp = f32x4{s8[0], s8[1], s8[2], s8[3]};
+    *(f32x4*)(sp + 4) = f32x4{s8[4], s8[5], s8[6], s8[7]};
+    *(f32x4*)(sp + CONV_BM) = f32x4{q8[0], q8[1], q8[2], q8[3]};
+    *(f32x4*)(sp + CONV_BM + 4) = f32x4{q8[4], q8[5], q8[6], q8[7]};
+  }
+  block_sync();  // E2
+  constexpr int SLOT = (NSEG == 1 ? 128 : 64);  // stat_slot_px(HW)
+  constexpr int WPS = SLOT / 64;                // halo waves per slot
+  for (int it = tt; it < (GNW_BN / SLOT) * CONV_BM; it += 256) {
+    const int sl = it / CONV_BM, cl = it % CONV_BM;
+    float sum = 0.f, sq = 0.f;
+#pragma unroll
+    for (int w = 0; w < WPS; ++w) {
+      sum += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + cl];
+      sq += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + CONV_BM + cl];
+    }
+    const long long slot = (long long)tileP / SLOT + sl;
+    a.stats[(slot * 2) * a.Cout + tileC + cl] = sum;
+    a.stats[(slot * 2 + 1) * a.Cout + tileC + cl] = sq;
+  }
+#ifdef ITSD_STAMPS
+  st[6] = stamp() - o0;
+#endif
+  WS_STAMP_OUT();
 }
 
 // Plain implicit-GEMM conv (conv_pipe's work: 3x3 stride 2, the 4x4 level's 3x3s, 1x1s) at
@@ -1412,6 +2079,418 @@ __global__ __launch_bounds__(512, 1) void splitk_wide_epilogue_kernel(ConvArgs a
   acc_to_E_wide(acc, (float*)smem);
   __syncthreads();
   epilogue_from_E<bf16_t, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
+}
+
+// ---------------------------------------------------------------------------- persistent, warp-specialized
+// conv3x3_gn_ws_kernel's stamps (profiles/r02_ws_stamps.txt): the MFMA waves keep the matrix pipe
+// ~88 % busy while they compute, but per 64-channel chunk they then wait ~5k cycles for the halo
+// waves (staging 14.5k cycles vs 10.5k of MFMA work: its 11 loads per lane are issued only when
+// the chunk starts), every tile begins with a ~10k-cycle exposed first-chunk staging, and ends with
+// a ~7k-cycle epilogue through a 128 KiB fp32 LDS tile. This kernel removes all three:
+//   * persistent: one block per CU walks the tiles t = blockIdx.x + k * gridDim.x; the 64-channel
+//     chunks of all its tiles form one stage sequence, double-buffered in LDS by stage parity;
+//   * halo waves (8..11) software-pipeline the stages: while transforming stage p they issue the
+//     loads of stage p+1 (item by item, into the registers just freed), so HBM latency hides
+//     behind a whole chunk; during a tile's last chunk they stage the NEXT tile's first chunk,
+//     copy this tile's residual rows into LDS (8-B units XOR-swizzled by row: conflict-free
+//     ds_read_b64 in the accumulator layout) and, during its first chunk, its bias/temb rows;
+//   * MFMA waves (0..7) run the epilogue straight from their accumulators: + addv + residual,
+//     one rounding, 8-B stores, and the consumer GroupNorm statistics by a butterfly over the 32
+//     pixel lanes -- each wave's 128 pixels are whole statistics slots and its 32 couts are its
+//     own, so the statistics go straight to the slab: no LDS tile, no block barrier. Meanwhile
+//     the halo waves already stage the next tile's second chunk.
+// A fragments are prefetched across chunk and tile boundaries (the 6-slot ring never drains).
+// Per output the MFMA sequence is conv3x3_gn_reg_kernel's.
+template <int W> struct GnpCfg;
+template <> struct GnpCfg<32> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
+template <> struct GnpCfg<16> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
+template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 0; };  // LDS: residual from HBM
+
+template <int W>
+__global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = GnpCfg<W>::ITEMS, RES = GnpCfg<W>::RES;
+  constexpr int W2 = W + 2;
+  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;
+  constexpr int HS = (THs + 2) * W2;
+  constexpr int TPS = 256 / NSEG, RPP = TPS / 8;
+  constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
+  constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
+  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4];
+  char* const rlds = smem + 2 * HALO;
+  float* const addv = (float*)(smem + 2 * HALO + RESB);  // [2 tile parities][NSEG][128]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.Hout;
+  const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
+  const int nTC = a.Cout / CONV_BM, NT = (a.M / GNW_BN) * nTC;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int ntiles = b < NT ? (NT - 1 - b) / G + 1 : 0;
+  const int nstages = ntiles * ncc;
+  auto tile_p = [&](int k) { return ((b + k * G) / nTC) * GNW_BN; };
+  auto tile_c = [&](int k) { return ((b + k * G) % nTC) * CONV_BM; };
+#ifdef ITSD_STAMPS
+  // MFMA waves: 0 chunk compute, 1 barrier wait, 6 epilogues, 7 total; halo waves: 3 stage
+  // transforms (incl. next-stage load issue), 1 barrier wait, 5 prologue (stage 0), 7 total
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_begin = stamp();
+  auto stamps_out = [&]() {
+    st[7] = stamp() - t_begin;
+    if (lane == 0) {
+      const int bb = blockIdx.x & 1023;
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) g_stamps[(bb * 16 + wid) * 8 + qq] = st[qq];
+    }
+  };
+#define PWS_STAMP_OUT() stamps_out()
+#else
+#define PWS_STAMP_OUT()
+#endif
+  auto block_sync = [&]() {
+    STAMP(b0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    STAMP(b1);
+    STAMP_ADD(1, b1 - b0);
+  };
+  if (ntiles == 0) return;  // (the host launches gridDim.x <= tiles)
+
+  if (wid < 8) {
+    // ================================================================ MFMA waves
+    const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
+    int hb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = wn * 128 + j * 32 + rl;
+      const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
+      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+    }
+    auto abase_of = [&](int k) {
+      return (const char*)a.wfrag + (size_t)((tile_c(k) >> 5) + wm) * (9 * kpt) * 1024 + lane * 16;
+    };
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    u32x4 ra[GNR_RING];
+    {
+      const char* ab0 = abase_of(0);
+#pragma unroll
+      for (int s0 = 0; s0 < GNR_RING - 1; ++s0)
+        ra[s0] = *(const u32x4*)(ab0 + (size_t)((s0 >> 2) * kpt + (s0 & 3)) * 1024);
+    }
+    block_sync();  // B0: stage 0 staged
+    int q = 0;     // stage (chunk) counter of this block
+    for (int k = 0; k < ntiles; ++k) {
+      const int tileP = tile_p(k), tileC = tile_c(k);
+      const char* ab = abase_of(k);
+      const char* abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
+      for (int cc = 0; cc < ncc; ++cc, ++q) {
+        const char* hcur = smem + (q & 1) * HALO;
+        // the next stage's A stream: this tile's next chunk, the next tile's first chunk, or
+        // (last stage) a harmless re-read of this chunk
+        const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 4 * 1024 : (k + 1 < ntiles ? abn : ab);
+        const char* cb = ab + (size_t)cc * 4 * 1024;
+        STAMP(c0);
+        // 36 k-steps (9 taps x 4): B fragments one k-step ahead, across tap boundaries; B fragment
+        // j of tap t sits at row h = hb[j] + toff(t), 16-B chunk (2kk + hh) ^ ((h >> 1) & 7), i.e.
+        // byte offset (h * 128 + ((hh ^ sw) << 4)) ^ (kk << 5) -- one XOR per read (the halo
+        // buffers are 128-B aligned, so the XOR only touches the chunk bits)
+        int bo[4];
+        auto tap_offsets = [&](int tap) {
+          const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int h = hb[j] + toff;
+            asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
+            bo[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+          }
+        };
+        bf16x8 fb[2][4];
+        auto rd = [&](int kk, int buf) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[buf][j] = *(const bf16x8*)(smem + (bo[j] ^ (kk << 5)));
+        };
+        tap_offsets(0);
+        rd(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int step = 0; step < 36; ++step) {
+          const int kk = step & 3;
+          const int pf = step + GNR_RING - 1;
+          if (pf < 36) ra[pf % GNR_RING] = *(const u32x4*)(cb + (size_t)((pf >> 2) * kpt + (pf & 3)) * 1024);
+          else ra[pf % GNR_RING] = *(const u32x4*)(nb + (size_t)(((pf - 36) >> 2) * kpt + ((pf - 36) & 3)) * 1024);
+          if (step + 1 < 36) {
+            if (kk == 3) tap_offsets((step + 1) >> 2);
+            rd((step + 1) & 3, (step + 1) & 1);
+          }
+          const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step & 1][j], acc[j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        STAMP(c1);
+        STAMP_ADD(0, c1 - c0);
+        block_sync();  // end of stage q: its buffer is free, stage q+1 is published
+      }
+      STAMP(e0);
+      // ---- epilogue of tile k from the accumulators (no LDS tile, no barrier)
+      // lane (rl, hh): pixels p_j = wn*128 + 32j + rl, couts c = wm*32 + 8g + 4hh + i
+      const float* av = addv + (k & 1) * NSEG * CONV_BM + wm * 32 + 4 * hh;
+      const bool has_res = a.resid != nullptr;
+      float s16[16], q16[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = wn * 128 + j * 32 + rl;
+        const float* avj = av + (NSEG == 1 ? 0 : (wn * 2 + (j >> 1))) * CONV_BM;
+        uint32_t wv[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = wm * 32 + 8 * g + 4 * hh;
+          const f32x4 ad = *(const f32x4*)(avj + 8 * g);
+          uint2 rr;
+          if constexpr (RES) {
+            rr = *(const uint2*)(rlds + p * 256 + (((c >> 2) ^ (p & 31)) * 8));
+          } else {
+            const T* rp = has_res ? (const T*)a.resid + (size_t)(tileP + p) * a.Cout + tileC + c
+                                  : (const T*)zero_of_block<T>(a);
+            rr = *(const uint2*)rp;
+          }
+          if (!has_res) rr = uint2{0u, 0u};  // select, not a branch
+          float v[4];
+          v[0] = acc[j][4 * g + 0] + ad[0] + __uint_as_float(rr.x << 16);
+          v[1] = acc[j][4 * g + 1] + ad[1] + __uint_as_float(rr.x & 0xffff0000u);
+          v[2] = acc[j][4 * g + 2] + ad[2] + __uint_as_float(rr.y << 16);
+          v[3] = acc[j][4 * g + 3] + ad[3] + __uint_as_float(rr.y & 0xffff0000u);
+          const T b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
+          wv[g][0] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+          wv[g][1] = (uint32_t)b2 | ((uint32_t)b3 << 16);
+          const float r0 = bf2f(b0), r1 = bf2f(b1), r2 = bf2f(b2), r3 = bf2f(b3);
+          s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
+          s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
+          s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
+          s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
+        }
+        // 16-B stores: v_permlane32_swap hands lane (rl, 0) its partner's upper couts of g0 and lane
+        // (rl, 1) its partner's lower couts of g1 -- each lane then owns 8 consecutive couts
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+          u32x4 o;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+            o[d] = sw[0];      // hh 0: own g0 lower;  hh 1: partner's g1 lower
+            o[2 + d] = sw[1];  // hh 0: partner's g0 upper;  hh 1: own g1 upper
+          }
+          const int c8 = wm * 32 + 8 * (gp + hh);
+          *(u32x4*)((T*)a.out + (size_t)(tileP + p) * a.Cout + tileC + c8) = o;
+        }
+        // statistics slot complete: W = 8 after every image (2 pixel tiles), else after all 4
+        if (a.stats && ((NSEG == 1 && j == 3) || (NSEG != 1 && (j & 1)))) {
+          // sum over the 32 pixel lanes of each half: DPP quad swaps, half-row / row mirrors,
+          // then a 16-lane swizzle (the two rows of the half)
+          auto sum32 = [](float v) {
+            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+            v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));
+            return v;
+          };
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            s16[e] = sum32(s16[e]);
+            q16[e] = sum32(q16[e]);
+          }
+          if (rl == 0) {
+            constexpr int SLOT = NSEG == 1 ? 128 : 64;
+            const long long slot = (long long)(tileP + wn * 128 + (NSEG == 1 ? 0 : (j >> 1) * 64)) / SLOT;
+            float* so = a.stats + (slot * 2) * a.Cout + tileC + wm * 32 + 4 * hh;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              *(f32x4*)(so + 8 * g) = f32x4{s16[4 * g], s16[4 * g + 1], s16[4 * g + 2], s16[4 * g + 3]};
+              *(f32x4*)(so + a.Cout + 8 * g) = f32x4{q16[4 * g], q16[4 * g + 1], q16[4 * g + 2], q16[4 * g + 3]};
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+      STAMP(e1);
+      STAMP_ADD(6, e1 - e0);
+    }
+    PWS_STAMP_OUT();
+    return;
+  }
+
+  // ================================================================== halo waves
+  const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
+  const T* zero = zero_of_block<T>(a);
+  struct Stage {
+    const T* src;
+    int Cs, cs0, img, y0;
+    const float* coef;
+  };
+  auto stage_of = [&](int p) {
+    Stage s;
+    const int k = p / ncc, cc = p - k * ncc;
+    const int tileP = tile_p(k);
+    const int img0 = tileP / (H * W);
+    s.img = img0 + sg;
+    s.y0 = (tileP - img0 * H * W) / W;
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    s.src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    s.Cs = s1 ? a.C1 : a.C2;
+    s.cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
+    s.coef = a.gn_coef + ((size_t)s.img * (Cin / 8) + cc * 8 + lch) * 16;
+    return s;
+  };
+  // Item geometry is recomputed from ltv, an opaque per-call copy of lt: the values are invariant
+  // across stages, and hoisted out of the stage loop the compiler spills them -- each reload a
+  // scratch load whose vmcnt wait also drains the next stage's prefetches.
+  int ltv = lt;
+  auto item_pix = [&](const Stage& s, int j) -> int {
+    const int r = (ltv >> 3) + RPP * j;
+    const int hy = r / W2, hx = r - hy * W2, iy = s.y0 + hy - 1, ix = hx - 1;
+    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    return ok ? (s.img * H + iy) * W + ix : -1;
+  };
+  auto item_lds = [&](int j) {
+    const int r = (ltv >> 3) + RPP * j;
+    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
+    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
+  };
+  auto load_item = [&](const Stage& s, int j) -> u32x4 {
+    const int po = item_pix(s, j);
+    return *(const u32x4*)(po >= 0 ? s.src + (unsigned)(po * s.Cs + s.cs0) : zero);
+  };
+  auto gn_silu1 = [](float x, float sc, float sh) {
+    const float y = x * sc + sh;
+    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
+  };
+  auto stage_addv = [&](int k) {
+    const int tileP = tile_p(k), tileC = tile_c(k), img0 = tileP / (H * W);
+    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+    for (int it = tt; it < NSEG * CONV_BM; it += 256) {
+      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
+      float v = a.bias[co];
+      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
+      if (a.cemb) {
+        int lab = 0;
+        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
+        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
+      }
+      addv[(k & 1) * NSEG * CONV_BM + it] = v;
+    }
+  };
+  // residual rows of tile k -> LDS, 4 groups of 4 x 16-B loads interleaved with the transform
+  u32x4 rq[4];
+  auto res_issue = [&](int k, int grp) {
+    const int tileP = tile_p(k), tileC = tile_c(k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tt >> 4) + 16 * (4 * grp + i);
+      rq[i] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + (tt & 15) * 8);
+    }
+  };
+  auto res_write = [&](int grp) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tt >> 4) + 16 * (4 * grp + i), u = 2 * (tt & 15);
+      *(uint2*)(rlds + row * 256 + ((u ^ (row & 31)) * 8)) = uint2{rq[i][0], rq[i][1]};
+      *(uint2*)(rlds + row * 256 + (((u + 1) ^ (row & 31)) * 8)) = uint2{rq[i][2], rq[i][3]};
+    }
+  };
+  u32x4 hreg[ITEMS];
+  f32x4 cf[4];
+  // transform stage p (its items are in hreg) into hbuf; as each item's register frees, the
+  // same item of stage p+1 is loaded into it; then stage p+1's coefficients. res_k >= 0: then
+  // also copy tile res_k's residual rows (after the transform: no registers held across it).
+  auto transform = [&](int p, char* hbuf, int res_k) {
+    ltv = lt;
+    asm volatile("" : "+v"(ltv));
+    const bool nxt = p + 1 < nstages;
+    const Stage sn = stage_of(nxt ? p + 1 : p);
+    const Stage sc = stage_of(p);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t* xw = (const uint32_t*)&hreg[j];
+      u32x4 y;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
+        const f32x4 avv = cf[w >> 1], bvv = cf[2 + (w >> 1)];
+        const int e = 2 * (w & 1);
+        const float r0 = gn_silu1(x0, avv[e], bvv[e]), r1 = gn_silu1(x1, avv[e + 1], bvv[e + 1]);
+        y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+      }
+      const bool pad = item_pix(sc, j) < 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
+      *(u32x4*)(hbuf + item_lds(j)) = y;
+      if (nxt) hreg[j] = load_item(sn, j);
+      // keep the item order: hoisting the next stage's loads above the transforms would
+      // need both stages' items live at once
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (nxt) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) cf[qq] = ((const f32x4*)sn.coef)[qq];
+    }
+    if (res_k >= 0) {
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        res_issue(res_k, grp);
+        res_write(grp);
+      }
+    }
+  };
+  // prologue: stage 0 (and tile 0's addv)
+  {
+    const Stage s0 = stage_of(0);
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) cf[qq] = ((const f32x4*)s0.coef)[qq];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) hreg[j] = load_item(s0, j);
+  }
+  stage_addv(0);
+  transform(0, smem, -1);
+#ifdef ITSD_STAMPS
+  st[5] = stamp() - t_begin;
+#endif
+  block_sync();  // B0
+  for (int q = 0; q < nstages; ++q) {  // during MFMA stage q
+    const int k = q / ncc, cc = q - k * ncc;
+    const int res_k = (RES && a.resid && cc == ncc - 1) ? k : -1;
+    if (cc == 0 && k > 0) stage_addv(k);
+    STAMP(h0);
+    if (q + 1 < nstages) transform(q + 1, smem + ((q + 1) & 1) * HALO, res_k);
+    else if (res_k >= 0) {
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {
+        res_issue(res_k, grp);
+        res_write(grp);
+      }
+    }
+#ifdef ITSD_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    STAMP(h1);
+    STAMP_ADD(3, h1 - h0);
+    block_sync();  // end of MFMA stage q
+  }
+  PWS_STAMP_OUT();
 }
 
 // GroupNorm finalize for the fused conv (the statistics half of gn_apply_kernel): per
@@ -1619,6 +2698,47 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     if (a.gn_coef) {
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
         const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+        if (g_gn_reg == 3 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
+            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
+          // persistent: one block per CU (160 KiB of LDS each), tiles strided over the grid
+          const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
+          const dim3 gp(std::min(tiles, g_num_cus));
+          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
+          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
+          else hipLaunchKernelGGL(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
+          return hipGetLastError();
+        }
+        if (g_gn_reg == 2 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
+            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
+          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
+          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
+          else hipLaunchKernelGGL(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
+          return hipGetLastError();
+        }
+        if (g_gn_reg && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
+            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
+          if ((g_conv_dbg & 4096) && a.Wout == 32) {  // measurement builds of the W = 32 kernel only
+            switch ((g_conv_dbg >> 13) & 127) {
+              case 1: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 1>), gw, dim3(512), 0, s, a); break;
+              case 2: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 2>), gw, dim3(512), 0, s, a); break;
+              case 4: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 4>), gw, dim3(512), 0, s, a); break;
+              case 8: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 8>), gw, dim3(512), 0, s, a); break;
+              case 16: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 16>), gw, dim3(512), 0, s, a); break;
+              case 6: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 6>), gw, dim3(512), 0, s, a); break;
+              case 14: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 14>), gw, dim3(512), 0, s, a); break;
+              case 30: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 30>), gw, dim3(512), 0, s, a); break;
+              case 24: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 24>), gw, dim3(512), 0, s, a); break;
+              case 32: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 32>), gw, dim3(512), 0, s, a); break;
+              case 64: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 64>), gw, dim3(512), 0, s, a); break;
+              default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+          }
+          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
+          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
+          else hipLaunchKernelGGL(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
+          return hipGetLastError();
+        }
         if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
         else hipLaunchKernelGGL(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
         return hipGetLastError();
@@ -1689,6 +2809,6 @@ template hipError_t launch_conv<bf16_t>(const ConvArgs&, hipStream_t);
 // diagnostic builds only: copy the wide fused conv's per-wave phase cycles out
 extern "C" int itsd_debug_stamps(unsigned long long* host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(itsd::g_stamps), sizeof(unsigned long long) * 1024 * 64) == hipSuccess ? 0 : 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(itsd::g_stamps), sizeof(unsigned long long) * 1024 * 128) == hipSuccess ? 0 : 1;
 }
 #endif
