@@ -1643,6 +1643,7 @@ template <int W> struct GnsCfg;
 template <> struct GnsCfg<32> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 10 x 34 halo rows
 template <> struct GnsCfg<16> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 18 x 18
 template <> struct GnsCfg<8> { static constexpr int NSEG = 4, ITEMS = 13; };   // 4 x 104 >= 4 x 10 x 10
+constexpr int GNS_MAXC = 896;  // input channels: 4 waves' GroupNorm coefficient tables fit behind the halos
 
 template <int W>
 __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
@@ -1798,67 +1799,126 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
   }
 
   // ================================================================== halo waves
+  // Item j of this thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch).
+  // Chunk-independent per item: the input pixel (0 for padding / scratch rows: a valid address
+  // whose value is never written) and whether the row is real input (okm) or zero padding inside
+  // the halo (padm; zeroed once in both buffers, never rewritten). Scratch rows past the segment
+  // are neither written nor read.
   const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
-  const T* zero = zero_of_block<T>(a);
-  auto item_row = [&](int j) { return (lt >> 3) + RPP * j; };
-  auto item_pix = [&](int j) -> int {
-    const int r = item_row(j);
+  const int hw = wid - 8;  // halo wave 0..3
+  int ipix[ITEMS];
+  uint32_t okm = 0, padm = 0;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int r = (lt >> 3) + RPP * j;
     const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    return ok ? ((img0 + sg) * H + iy) * W + ix : -1;
+    const bool in = iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const bool ok = r < HS && in;
+    ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
+    okm |= (uint32_t)ok << j;
+    padm |= (uint32_t)(r < HS && !in) << j;
+  }
+  // LDS byte offset of item j in buffer 0: row h = sg*HS + r, 16-B chunk lch swizzled by (h>>1)&7;
+  // with RPP a multiple of 16 the swizzle is the same for every item, with RPP = 8 it alternates
+  const int hrow0 = sg * HS + (lt >> 3), hrow1 = hrow0 + RPP;
+  const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
+  const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
+  auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
+  static_assert(HROWS > NSEG * HS, "a scratch row exists");
+  const int dump = NSEG * HS * ROWB + (lch << 4);  // never read
+  // GroupNorm coefficient table of this wave's image (every chunk: 8 lanes' a[8], b[8]), private to
+  // the wave (its own writes, no barrier), in the E area behind the halos until the epilogue
+  float* const ctab = (float*)(smem + 2 * HALO) + hw * (GNS_MAXC / 8) * 16;
+  static_assert(2 * HALO + 4 * (GNS_MAXC / 8) * 64 <= GNW_BN * EROW * 4, "coefficient tables lie under E");
+  {
+    constexpr int NP = (GNS_MAXC / 8) * 4 / 64;  // 16-B pieces per lane at most
+    const int nent = ncc * 8 * 4;
+    const f32x4* src = (const f32x4*)(a.gn_coef + (size_t)(img0 + (NSEG == 1 ? 0 : hw)) * (Cin / 8) * 16);
+    f32x4 tp[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      if (lane + 64 * k < nent) tp[k] = src[lane + 64 * k];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      if (lane + 64 * k < nent) *(f32x4*)(ctab + (lane + 64 * k) * 4) = tp[k];
+  }
+  // Chunk cc's item j: a buffer load (32-bit byte offset into its source -- src1, or src2, the
+  // concatenated skip input -- the chunk's channel offset in soffset; past the last chunk a
+  // zero-record descriptor: the load returns 0 and touches no memory, so every reload is
+  // unconditional). Item j's register is reloaded with the next chunk's item j right after its
+  // transform: ITEMS loads stay in flight, each for about one MFMA chunk before its use.
+  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
+  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
+  struct ChunkSrc {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t rowb, so;
   };
-  auto item_lds = [&](int j) {
-    const int r = item_row(j);
-    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
-    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
-  };
-  auto gn_silu1 = [](float x, float sc, float sh) {
-    const float y = x * sc + sh;
-    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
-  };
-  // one chunk's halo: all item loads in flight, then transform + LDS write item by item
-  auto stage_chunk = [&](int cc, char* hbuf) {
+  auto chunk_src = [&](int cc) __attribute__((always_inline)) {  // scalar selects only (uniform)
     const int ci0 = cc * 64;
     const bool s1 = ci0 < a.C1;
-    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
-    const int Cs = s1 ? a.C1 : a.C2;
-    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
-    u32x4 hreg[ITEMS];
+    ChunkSrc c;
+    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0,
+                                             s1 ? nrec1 : (ci0 < Cin ? nrec2 : 0), 0x00020000);
+    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
+    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
+    return c;
+  };
+  u32x4 h[ITEMS];
+  auto load_item = [&](const ChunkSrc& c, int j) __attribute__((always_inline)) {
+    h[j] = __builtin_amdgcn_raw_buffer_load_b128(c.rs, __umul24((uint32_t)ipix[j], c.rowb) + lch * 16, c.so, 0);
+  };
+  // silu(x*a + b) per channel pair (same operations as gn_silu2: fma, exp2(-log2e*y), +1, rcp,
+  // mul), rounded to a bf16 pair; written to the LDS halo where the row is real input
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  auto emit = [&](int cc, char* hbuf) __attribute__((always_inline)) {
+    f32x4 c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = *(const f32x4*)(ctab + (cc * 8 + lch) * 16 + q * 4);
+    const ChunkSrc nx = chunk_src(cc + 1);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const int po = item_pix(j);
-      hreg[j] = *(const u32x4*)(po >= 0 ? src + (unsigned)(po * Cs + cs0) : zero);
-    }
-    f32x4 cf[4];
-    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cf[q] = cp[q];
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const uint32_t* xw = (const uint32_t*)&hreg[j];
       u32x4 y;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
-        const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
+        // scalar f32 (packed f32 VALU beside MFMAs costs ~22 cycles an instruction,
+        // MI355X_MICROARCH.md 'price of one filler'; the file is built without SLP packing)
+        const uint32_t xw = h[j][w];
         const int e = 2 * (w & 1);
-        const float r0 = gn_silu1(x0, av[e], bv[e]), r1 = gn_silu1(x1, av[e + 1], bv[e + 1]);
-        y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+        const float v0 = __builtin_fmaf(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
+        const float v1 = __builtin_fmaf(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
+        const float s0 = v0 * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v0 * -1.44269502f) + 1.0f);
+        const float s1 = v1 * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v1 * -1.44269502f) + 1.0f);
+        y[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{s0, s1}, bf16x2_t));
       }
-      const bool pad = item_pix(j) < 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
-      *(u32x4*)(hbuf + item_lds(j)) = y;
+      // the reload strictly after the transform (same basic block: the store below is not
+      // conditional -- rows that are not real input go to a scratch row -- so the transform is
+      // not sunk under a branch behind the reload, which costs a second register set + copies)
+      *(u32x4*)(hbuf + (((okm >> j) & 1) ? item_lds(j) : dump)) = y;
+      __builtin_amdgcn_sched_barrier(0);
+      load_item(nx, j);
     }
   };
-  stage_chunk(0, smem);
+  {
+    const ChunkSrc c0 = chunk_src(0);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) load_item(c0, j);
+  }
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if ((padm >> j) & 1) {
+      *(u32x4*)(smem + item_lds(j)) = u32x4{0u, 0u, 0u, 0u};
+      *(u32x4*)(smem + HALO + item_lds(j)) = u32x4{0u, 0u, 0u, 0u};
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's coefficient table is written
+  emit(0, smem);
 #ifdef ITSD_STAMPS
   st[5] = stamp() - t_begin;
 #endif
   block_sync();  // B0
   for (int cc = 0; cc + 1 < ncc; ++cc) {
     STAMP(h0);
-    stage_chunk(cc + 1, smem + ((cc + 1) & 1) * HALO);
+    emit(cc + 1, smem + ((cc + 1) & 1) * HALO);  // while the MFMA waves compute chunk cc
 #ifdef ITSD_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -1925,7 +1985,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
     s8[e] += __shfl_xor(s8[e], 32, 64);
     q8[e] += __shfl_xor(q8[e], 32, 64);
   }
-  const int hw = wid - 8;  // halo wave 0..3: rows 64*hw .. +63
+  // halo wave hw: rows 64*hw .. +63
   if (lane < 16) {
     float* sp = spart + (size_t)hw * 2 * CONV_BM + ecq * 8;
     *(f32x4*)sp = f32x4{s8[0], s8[1], s8[2], s8[3]};
@@ -2708,7 +2768,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           else hipLaunchKernelGGL(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
           return hipGetLastError();
         }
-        if (g_gn_reg == 2 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
+        if (g_gn_reg == 2 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 <= GNS_MAXC &&
             (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
           if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
           else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);

@@ -16,7 +16,8 @@ import torch
 from .arch import ARCH_CFG, ARCH_DDPM, UNetArch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libitsd_hip.so")
+# ITSD_LIB: an alternative build of the same library (diagnostic A/B builds under build_diag/)
+LIB_PATH = os.environ.get("ITSD_LIB") or os.path.join(_HERE, "libitsd_hip.so")
 
 ITSD_OK, ITSD_ERR_INVALID, ITSD_ERR_HIP, ITSD_ERR_WEIGHTS, ITSD_ERR_NAN, ITSD_ERR_OOM = range(6)
 PREC_FP32, PREC_BF16 = 0, 1
