@@ -915,7 +915,8 @@ int itsd_set_option(const char* key, int value) {
     // fused conv) every lane reads the same B / A fragment row (LDS broadcast). (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
     // 4096 | (mask << 13): compile-time ablations of conv3x3_gn_reg_kernel<32> (conv.hip)
-    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13));
+    // (1 << 20) / (1 << 21): s_setprio 1 / 2 for the halo waves of the ws / pws fused GroupNorm convs
+    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13) | (3 << 20));
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {

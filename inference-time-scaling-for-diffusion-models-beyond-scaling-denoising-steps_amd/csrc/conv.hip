@@ -43,7 +43,7 @@ int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
-int g_gn_reg = 2;        // fused GroupNorm conv with the weights streamed into registers where the
+int g_gn_reg = 3;        // fused GroupNorm conv with the weights streamed into registers where the
                          // 256-pixel tile applies: 0 off, 1 conv3x3_gn_reg_kernel, 2 warp-specialized
                          // conv3x3_gn_ws_kernel (halo waves), 3 persistent conv3x3_gn_pws_kernel
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
@@ -1639,6 +1639,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_reg_kernel(ConvArgs a) {
 //     concurrently on a SIMD), prefetch the residual rows during the last chunk, and run the
 //     epilogue's output pass (+ bias/temb/residual, rounding, 16-B stores, GroupNorm statistics).
 // 3 waves per SIMD: 168 VGPRs each. The MFMA sequence per output equals the register kernel's.
+// silu(x*a + b) from coefficients prescaled by -log2(e) (a' = -a log2e, b' = -b log2e):
+// t = x a' + b' = -y log2e, 2^t = e^-y, and silu(y) = y / (1 + e^-y) = t / ((1 + 2^t)(-1/ln2))
+// -- fma, exp2, fma, rcp, mul: one VALU op fewer than fma, mul, exp2, add, rcp, mul
+constexpr float GN_L2E = -1.44269504f;
+__device__ __forceinline__ float gn_silu_l2(float x, float a2, float b2) {
+  const float t = __builtin_fmaf(x, a2, b2);
+  return t * __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(t), GN_L2E, GN_L2E));
+}
 template <int W> struct GnsCfg;
 template <> struct GnsCfg<32> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 10 x 34 halo rows
 template <> struct GnsCfg<16> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 18 x 18
@@ -1806,6 +1814,9 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
   // are neither written nor read.
   const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
   const int hw = wid - 8;  // halo wave 0..3
+  // measurement switch (conv_dbg bit 20 / 21): static priority 1 / 2 for the halo waves
+  if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);
+  if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
   int ipix[ITEMS];
   uint32_t okm = 0, padm = 0;
 #pragma unroll
@@ -1840,7 +1851,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
       if (lane + 64 * k < nent) tp[k] = src[lane + 64 * k];
 #pragma unroll
     for (int k = 0; k < NP; ++k)
-      if (lane + 64 * k < nent) *(f32x4*)(ctab + (lane + 64 * k) * 4) = tp[k];
+      if (lane + 64 * k < nent) *(f32x4*)(ctab + (lane + 64 * k) * 4) = tp[k] * GN_L2E;  // prescaled: gn_silu_l2
   }
   // Chunk cc's item j: a buffer load (32-bit byte offset into its source -- src1, or src2, the
   // concatenated skip input -- the chunk's channel offset in soffset; past the last chunk a
@@ -1885,10 +1896,8 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
         // MI355X_MICROARCH.md 'price of one filler'; the file is built without SLP packing)
         const uint32_t xw = h[j][w];
         const int e = 2 * (w & 1);
-        const float v0 = __builtin_fmaf(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
-        const float v1 = __builtin_fmaf(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
-        const float s0 = v0 * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v0 * -1.44269502f) + 1.0f);
-        const float s1 = v1 * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v1 * -1.44269502f) + 1.0f);
+        const float s0 = gn_silu_l2(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
+        const float s1 = gn_silu_l2(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
         y[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{s0, s1}, bf16x2_t));
       }
       // the reload strictly after the transform (same basic block: the store below is not
@@ -2149,11 +2158,12 @@ __global__ __launch_bounds__(512, 1) void splitk_wide_epilogue_kernel(ConvArgs a
 // a ~7k-cycle epilogue through a 128 KiB fp32 LDS tile. This kernel removes all three:
 //   * persistent: one block per CU walks the tiles t = blockIdx.x + k * gridDim.x; the 64-channel
 //     chunks of all its tiles form one stage sequence, double-buffered in LDS by stage parity;
-//   * halo waves (8..11) software-pipeline the stages: while transforming stage p they issue the
-//     loads of stage p+1 (item by item, into the registers just freed), so HBM latency hides
-//     behind a whole chunk; during a tile's last chunk they stage the NEXT tile's first chunk,
-//     copy this tile's residual rows into LDS (8-B units XOR-swizzled by row: conflict-free
-//     ds_read_b64 in the accumulator layout) and, during its first chunk, its bias/temb rows;
+//   * halo waves (8..11) software-pipeline the stages as conv3x3_gn_ws_kernel's do: while
+//     transforming stage p they reload each item's register with stage p+1's item right after its
+//     transform, so HBM latency hides behind a whole chunk; during a tile's last chunk they stage
+//     the NEXT tile's first chunk and LDS-DMA this tile's residual rows into LDS (16-B units
+//     XOR-swizzled by row: conflict-free 8-B reads in the accumulator layout), and with its first
+//     chunk write its bias/temb rows;
 //   * MFMA waves (0..7) run the epilogue straight from their accumulators: + addv + residual,
 //     one rounding, 8-B stores, and the consumer GroupNorm statistics by a butterfly over the 32
 //     pixel lanes -- each wave's 128 pixels are whole statistics slots and its 32 couts are its
@@ -2316,7 +2326,7 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
           const f32x4 ad = *(const f32x4*)(avj + 8 * g);
           uint2 rr;
           if constexpr (RES) {
-            rr = *(const uint2*)(rlds + p * 256 + (((c >> 2) ^ (p & 31)) * 8));
+            rr = *(const uint2*)(rlds + p * 256 + ((((c >> 3) ^ (p & 15)) << 4) | ((c & 4) << 1)));
           } else {
             const T* rp = has_res ? (const T*)a.resid + (size_t)(tileP + p) * a.Cout + tileC + c
                                   : (const T*)zero_of_block<T>(a);
@@ -2353,30 +2363,46 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
         }
         // statistics slot complete: W = 8 after every image (2 pixel tiles), else after all 4
         if (a.stats && ((NSEG == 1 && j == 3) || (NSEG != 1 && (j & 1)))) {
-          // sum over the 32 pixel lanes of each half: DPP quad swaps, half-row / row mirrors,
-          // then a 16-lane swizzle (the two rows of the half)
-          auto sum32 = [](float v) {
-            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-            v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-            v += __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F));
-            return v;
-          };
+          // sums over the 32 pixel lanes of each half by recursive halving: at the step of
+          // width w (16, 8, 4, 2, 1) a lane keeps the upper or lower w of its values by bit w of
+          // rl and adds its xor-w partner's copy of them -- 31 exchanges instead of 5 x 32. Lane rl
+          // ends with value rl: s16[rl] (rl < 16) or q16[rl - 16]. Exchanges: DPP quad_perm (1, 2),
+          // row_ror:8 (8), ds_swizzle xor (4, 16).
+          float v[32];
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            s16[e] = sum32(s16[e]);
-            q16[e] = sum32(q16[e]);
+            v[e] = s16[e];
+            v[16 + e] = q16[e];
           }
-          if (rl == 0) {
+          auto xchg = [](float x, auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const int xi = __builtin_bit_cast(int, x);
+            int r;
+            if constexpr (w == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+            else if constexpr (w == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+            else if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+            else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (w << 10));
+            return __builtin_bit_cast(float, r);
+          };
+          auto halve = [&](auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const bool up = (rl & w) != 0;
+#pragma unroll
+            for (int i = 0; i < w; ++i) {
+              const float lo = v[i], hi = v[i + w];
+              v[i] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+            }
+          };
+          halve(std::integral_constant<int, 16>{});
+          halve(std::integral_constant<int, 8>{});
+          halve(std::integral_constant<int, 4>{});
+          halve(std::integral_constant<int, 2>{});
+          halve(std::integral_constant<int, 1>{});
+          {
             constexpr int SLOT = NSEG == 1 ? 128 : 64;
             const long long slot = (long long)(tileP + wn * 128 + (NSEG == 1 ? 0 : (j >> 1) * 64)) / SLOT;
-            float* so = a.stats + (slot * 2) * a.Cout + tileC + wm * 32 + 4 * hh;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              *(f32x4*)(so + 8 * g) = f32x4{s16[4 * g], s16[4 * g + 1], s16[4 * g + 2], s16[4 * g + 3]};
-              *(f32x4*)(so + a.Cout + 8 * g) = f32x4{q16[4 * g], q16[4 * g + 1], q16[4 * g + 2], q16[4 * g + 3]};
-            }
+            const int e = rl & 15, co = wm * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+            a.stats[(slot * 2 + (rl >> 4)) * a.Cout + tileC + co] = v[0];
           }
 #pragma unroll
           for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
@@ -2394,50 +2420,62 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
   }
 
   // ================================================================== halo waves
+  // (conv3x3_gn_ws_kernel's halo pipeline, over the block's whole stage sequence.) Item j of this
+  // thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch). Per tile: the
+  // input pixel of each item (0 for padding / scratch rows: a valid address, never used) for the
+  // loads, and per item whether the row is real input (okm), zero padding inside the halo (padm;
+  // written as zeros every stage: the padding rows differ between tiles) or scratch (neither:
+  // written to a dump row that is never read).
   const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
-  const T* zero = zero_of_block<T>(a);
-  struct Stage {
-    const T* src;
-    int Cs, cs0, img, y0;
-    const float* coef;
+  static_assert(NSEG * ITEMS * RPP > NSEG * HS, "a scratch row exists");
+  if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);  // measurement switches, as in the ws kernel
+  if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
+  const int dump = NSEG * HS * ROWB + (lch << 4);
+  const int hrow0 = sg * HS + (lt >> 3), hrow1 = hrow0 + RPP;
+  const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
+  const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
+  auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
+  int ipix[ITEMS];
+  uint32_t okmL = 0, padmL = 0;  // masks of the tile being loaded
+  auto geometry = [&](int k) __attribute__((always_inline)) {
+    const int tileP = tile_p(k), img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
+    okmL = padmL = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int r = (lt >> 3) + RPP * j;
+      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+      const bool in = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const bool ok = r < HS && in;
+      ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
+      okmL |= (uint32_t)ok << j;
+      padmL |= (uint32_t)(r < HS && !in) << j;
+    }
   };
-  auto stage_of = [&](int p) {
-    Stage s;
-    const int k = p / ncc, cc = p - k * ncc;
-    const int tileP = tile_p(k);
-    const int img0 = tileP / (H * W);
-    s.img = img0 + sg;
-    s.y0 = (tileP - img0 * H * W) / W;
-    const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
-    s.src = s1 ? (const T*)a.src1 : (const T*)a.src2;
-    s.Cs = s1 ? a.C1 : a.C2;
-    s.cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
-    s.coef = a.gn_coef + ((size_t)s.img * (Cin / 8) + cc * 8 + lch) * 16;
-    return s;
+  // stage p's item loads: buffer loads (32-bit byte offset into src1, or src2 = the concatenated
+  // skip input; the chunk's channel offset in soffset); past the last stage a zero-record
+  // descriptor, so every reload is unconditional (a conditional one keeps the old value alive
+  // beside the new one: a second register set the compiler rotates with waiting copies)
+  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
+  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
+  struct Src {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t rowb, so;
   };
-  // Item geometry is recomputed from ltv, an opaque per-call copy of lt: the values are invariant
-  // across stages, and hoisted out of the stage loop the compiler spills them -- each reload a
-  // scratch load whose vmcnt wait also drains the next stage's prefetches.
-  int ltv = lt;
-  auto item_pix = [&](const Stage& s, int j) -> int {
-    const int r = (ltv >> 3) + RPP * j;
-    const int hy = r / W2, hx = r - hy * W2, iy = s.y0 + hy - 1, ix = hx - 1;
-    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    return ok ? (s.img * H + iy) * W + ix : -1;
+  auto src_of = [&](int p) __attribute__((always_inline)) {  // scalar selects only (uniform)
+    const int k = p / ncc, ci0 = (p - k * ncc) * 64;
+    const bool s1 = ci0 < a.C1, live = p < nstages;
+    Src c;
+    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0,
+                                             live ? (s1 ? nrec1 : nrec2) : 0, 0x00020000);
+    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
+    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
+    return c;
   };
-  auto item_lds = [&](int j) {
-    const int r = (ltv >> 3) + RPP * j;
-    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
-    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
-  };
-  auto load_item = [&](const Stage& s, int j) -> u32x4 {
-    const int po = item_pix(s, j);
-    return *(const u32x4*)(po >= 0 ? s.src + (unsigned)(po * s.Cs + s.cs0) : zero);
-  };
-  auto gn_silu1 = [](float x, float sc, float sh) {
-    const float y = x * sc + sh;
-    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
+  auto coef_of = [&](int p) __attribute__((always_inline)) {
+    const int pp = p < nstages ? p : nstages - 1;
+    const int k = pp / ncc, cc = pp - k * ncc;
+    const int img = tile_p(k) / (H * W) + sg;
+    return (const f32x4*)(a.gn_coef + ((size_t)img * (Cin / 8) + cc * 8 + lch) * 16);
   };
   auto stage_addv = [&](int k) {
     const int tileP = tile_p(k), tileC = tile_c(k), img0 = tileP / (H * W);
@@ -2454,95 +2492,88 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
       addv[(k & 1) * NSEG * CONV_BM + it] = v;
     }
   };
-  // residual rows of tile k -> LDS, 4 groups of 4 x 16-B loads interleaved with the transform
-  u32x4 rq[4];
-  auto res_issue = [&](int k, int grp) {
-    const int tileP = tile_p(k), tileC = tile_c(k);
+  // residual rows of tile k -> LDS by LDS-DMA (16 B a lane, 1 KiB a wave-instruction, no
+  // registers): row p, 16-B unit u of its 256 B lands at unit u ^ (p & 15) (source-side inverse
+  // swizzle), which the MFMA waves' 8-B reads in the accumulator layout hit conflict-free
+  auto res_dma = [&](int k) __attribute__((always_inline)) {
+    if constexpr (RES) {
+      const int tileP = tile_p(k), tileC = tile_c(k), hw = wid - 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (tt >> 4) + 16 * (4 * grp + i);
-      rq[i] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + (tt & 15) * 8);
+      for (int i = 0; i < 16; ++i) {  // wave hw: rows 64*hw + 4*i .. +3, lane -> (row, slot)
+        const int row = 64 * hw + 4 * i + (lane >> 4), slot = lane & 15, u = slot ^ (row & 15);
+        const T* src = (const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + u * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(rlds + (64 * hw + 4 * i) * 256), 16, 0, 0);
+      }
     }
   };
-  auto res_write = [&](int grp) {
+  u32x4 h[ITEMS];
+  f32x4 c[4], cn[4];
+  // transform stage p (items in h, coefficients in c) into hbuf; each item's register is reloaded
+  // with stage p+1's item right after its transform, stage p+1's coefficients go to cn first
+  // (older than every item reload: waiting for them never waits for an item). The masks are
+  // tile(p)'s; the reloads use tile(p+1)'s geometry.
+  auto emit = [&](int p, char* hbuf) __attribute__((always_inline)) {
+    const uint32_t okm = okmL, padm = padmL;
+    const int kn = (p + 1) / ncc;
+    if (p + 1 < nstages && kn != p / ncc) geometry(kn);
+    const f32x4* cp = coef_of(p + 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (tt >> 4) + 16 * (4 * grp + i), u = 2 * (tt & 15);
-      *(uint2*)(rlds + row * 256 + ((u ^ (row & 31)) * 8)) = uint2{rq[i][0], rq[i][1]};
-      *(uint2*)(rlds + row * 256 + (((u + 1) ^ (row & 31)) * 8)) = uint2{rq[i][2], rq[i][3]};
-    }
-  };
-  u32x4 hreg[ITEMS];
-  f32x4 cf[4];
-  // transform stage p (its items are in hreg) into hbuf; as each item's register frees, the
-  // same item of stage p+1 is loaded into it; then stage p+1's coefficients. res_k >= 0: then
-  // also copy tile res_k's residual rows (after the transform: no registers held across it).
-  auto transform = [&](int p, char* hbuf, int res_k) {
-    ltv = lt;
-    asm volatile("" : "+v"(ltv));
-    const bool nxt = p + 1 < nstages;
-    const Stage sn = stage_of(nxt ? p + 1 : p);
-    const Stage sc = stage_of(p);
+    for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+    const Src nx = src_of(p + 1);
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const uint32_t* xw = (const uint32_t*)&hreg[j];
       u32x4 y;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
-        const f32x4 avv = cf[w >> 1], bvv = cf[2 + (w >> 1)];
+        const uint32_t xw = h[j][w];
         const int e = 2 * (w & 1);
-        const float r0 = gn_silu1(x0, avv[e], bvv[e]), r1 = gn_silu1(x1, avv[e + 1], bvv[e + 1]);
-        y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
+        const float s0 = gn_silu_l2(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
+        const float s1 = gn_silu_l2(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
+        y[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{s0, s1}, bf16x2_t));
       }
-      const bool pad = item_pix(sc, j) < 0;
+      const bool ok = (okm >> j) & 1, keep = ok || ((padm >> j) & 1);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
-      *(u32x4*)(hbuf + item_lds(j)) = y;
-      if (nxt) hreg[j] = load_item(sn, j);
-      // keep the item order: hoisting the next stage's loads above the transforms would
-      // need both stages' items live at once
+      for (int e = 0; e < 4; ++e) y[e] = ok ? y[e] : 0u;
+      *(u32x4*)(hbuf + (keep ? item_lds(j) : dump)) = y;
       __builtin_amdgcn_sched_barrier(0);
+      h[j] = __builtin_amdgcn_raw_buffer_load_b128(nx.rs, __umul24((uint32_t)ipix[j], nx.rowb) + lch * 16, nx.so, 0);
     }
-    if (nxt) {
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) cf[qq] = ((const f32x4*)sn.coef)[qq];
-    }
-    if (res_k >= 0) {
-#pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
-        res_issue(res_k, grp);
-        res_write(grp);
-      }
-    }
+    for (int q = 0; q < 4; ++q) c[q] = cn[q] * GN_L2E;  // prescaled: gn_silu_l2
   };
   // prologue: stage 0 (and tile 0's addv)
+  geometry(0);
   {
-    const Stage s0 = stage_of(0);
+    const f32x4* cp = coef_of(0);
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) cf[qq] = ((const f32x4*)s0.coef)[qq];
+    for (int q = 0; q < 4; ++q) c[q] = cp[q] * GN_L2E;
+    const Src s0 = src_of(0);
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) hreg[j] = load_item(s0, j);
+    for (int j = 0; j < ITEMS; ++j)
+      h[j] = __builtin_amdgcn_raw_buffer_load_b128(s0.rs, __umul24((uint32_t)ipix[j], s0.rowb) + lch * 16, s0.so, 0);
   }
   stage_addv(0);
-  transform(0, smem, -1);
+  emit(0, smem);
 #ifdef ITSD_STAMPS
   st[5] = stamp() - t_begin;
 #endif
   block_sync();  // B0
   for (int q = 0; q < nstages; ++q) {  // during MFMA stage q
     const int k = q / ncc, cc = q - k * ncc;
-    const int res_k = (RES && a.resid && cc == ncc - 1) ? k : -1;
-    if (cc == 0 && k > 0) stage_addv(k);
     STAMP(h0);
-    if (q + 1 < nstages) transform(q + 1, smem + ((q + 1) & 1) * HALO, res_k);
-    else if (res_k >= 0) {
-#pragma unroll
-      for (int grp = 0; grp < 4; ++grp) {
-        res_issue(res_k, grp);
-        res_write(grp);
-      }
+    // tile k's residual, during its last chunk (issued before the item reloads: the wait below
+    // for it leaves them in flight); tile k+1's addv with its first chunk
+    const bool res = RES && a.resid && cc == ncc - 1;
+    if (res) res_dma(k);
+    if (q + 1 < nstages) {
+      if ((q + 1) % ncc == 0) stage_addv((q + 1) / ncc);
+      emit(q + 1, smem + ((q + 1) & 1) * HALO);
     }
+    // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
+    // issued after it, may still be in flight)
+    if (res) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
 #ifdef ITSD_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
