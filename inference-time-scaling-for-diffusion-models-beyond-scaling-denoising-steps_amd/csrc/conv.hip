@@ -1647,6 +1647,49 @@ __device__ __forceinline__ float gn_silu_l2(float x, float a2, float b2) {
   const float t = __builtin_fmaf(x, a2, b2);
   return t * __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_amdgcn_exp2f(t), GN_L2E, GN_L2E));
 }
+// Two packed bf16 pairs (4 channels) through gn_silu_l2, rounded back to bf16 pairs and masked
+// (zm: 0 zeroes a padding row) -- the halo waves' transform as one fixed instruction stream: four
+// independent chains interleaved, so no transcendental's consumer follows it directly (no
+// hazard s_nop) and exp / rcp latency overlaps. The compiler, at this kernel's register
+// pressure, scheduled the same work one chain at a time with a nop after every v_exp / v_rcp.
+__device__ __forceinline__ void gn_silu_x4(uint32_t xa, uint32_t xb, float a0, float a1, float a2, float a3,
+                                           float b0, float b1, float b2, float b3, uint32_t zm, uint32_t& ya,
+                                           uint32_t& yb) {
+  float t0, t1, t2, t3, e0, e1, e2, e3;
+  asm volatile(
+      "v_lshlrev_b32 %2, 16, %10\n\t"
+      "v_and_b32 %3, 0xffff0000, %10\n\t"
+      "v_lshlrev_b32 %4, 16, %11\n\t"
+      "v_and_b32 %5, 0xffff0000, %11\n\t"
+      "v_fma_f32 %2, %2, %12, %16\n\t"
+      "v_fma_f32 %3, %3, %13, %17\n\t"
+      "v_fma_f32 %4, %4, %14, %18\n\t"
+      "v_fma_f32 %5, %5, %15, %19\n\t"
+      "v_exp_f32 %6, %2\n\t"
+      "v_exp_f32 %7, %3\n\t"
+      "v_exp_f32 %8, %4\n\t"
+      "v_exp_f32 %9, %5\n\t"
+      "v_fma_f32 %6, %6, %21, %21\n\t"
+      "v_fma_f32 %7, %7, %21, %21\n\t"
+      "v_fma_f32 %8, %8, %21, %21\n\t"
+      "v_fma_f32 %9, %9, %21, %21\n\t"
+      "v_rcp_f32 %6, %6\n\t"
+      "v_rcp_f32 %7, %7\n\t"
+      "v_rcp_f32 %8, %8\n\t"
+      "v_rcp_f32 %9, %9\n\t"
+      "v_mul_f32 %2, %2, %6\n\t"
+      "v_mul_f32 %3, %3, %7\n\t"
+      "v_mul_f32 %4, %4, %8\n\t"
+      "v_mul_f32 %5, %5, %9\n\t"
+      "v_cvt_pk_bf16_f32 %0, %2, %3\n\t"
+      "v_cvt_pk_bf16_f32 %1, %4, %5\n\t"
+      "v_and_b32 %0, %0, %20\n\t"
+      "v_and_b32 %1, %1, %20"
+      : "=&v"(ya), "=&v"(yb), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(e0), "=&v"(e1), "=&v"(e2),
+        "=&v"(e3)
+      : "v"(xa), "v"(xb), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(zm),
+        "s"(GN_L2E));
+}
 template <int W> struct GnsCfg;
 template <> struct GnsCfg<32> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 10 x 34 halo rows
 template <> struct GnsCfg<16> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 18 x 18
@@ -2421,11 +2464,11 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
 
   // ================================================================== halo waves
   // (conv3x3_gn_ws_kernel's halo pipeline, over the block's whole stage sequence.) Item j of this
-  // thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch). Per tile: the
-  // input pixel of each item (0 for padding / scratch rows: a valid address, never used) for the
-  // loads, and per item whether the row is real input (okm), zero padding inside the halo (padm;
-  // written as zeros every stage: the padding rows differ between tiles) or scratch (neither:
-  // written to a dump row that is never read).
+  // thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch). Per tile, for
+  // the loads: the input pixel of each item (0 for padding / scratch rows: a valid address,
+  // never used); for the LDS writes: each item's address (its halo row, or a dump row past the
+  // segments for scratch rows) and a mask that zeroes padding rows (rewritten every stage: the
+  // padding rows differ between tiles). Stage and tile indices advance by counters (no divides).
   const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
   static_assert(NSEG * ITEMS * RPP > NSEG * HS, "a scratch row exists");
   if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);  // measurement switches, as in the ws kernel
@@ -2435,47 +2478,68 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
   const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
   const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
   auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
+  auto tile_y0img = [&](int k, int& img0, int& y0) {
+    const int tileP = tile_p(k);
+    img0 = tileP / (H * W);
+    y0 = (tileP - img0 * H * W) / W;
+  };
   int ipix[ITEMS];
-  uint32_t okmL = 0, padmL = 0;  // masks of the tile being loaded
-  auto geometry = [&](int k) __attribute__((always_inline)) {
-    const int tileP = tile_p(k), img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
-    okmL = padmL = 0;
+  const float* cbase;  // GroupNorm coefficients of the loading tile's image, this lane's 8 channels
+  auto geometry_pix = [&](int k) __attribute__((always_inline)) {
+    int img0, y0;
+    tile_y0img(k, img0, y0);
+    // the item geometry from an opaque copy of lt: hoisted out of the stage loop (it is tile-
+    // invariant), it would hold ~30 registers for good and starve the transform of temporaries
+    int ltv = lt;
+    asm volatile("" : "+v"(ltv));
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const int r = (lt >> 3) + RPP * j;
+      const int r = (ltv >> 3) + RPP * j;
       const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-      const bool in = iy >= 0 && iy < H && ix >= 0 && ix < W;
-      const bool ok = r < HS && in;
+      const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
       ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
-      okmL |= (uint32_t)ok << j;
-      padmL |= (uint32_t)(r < HS && !in) << j;
+    }
+    cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
+  };
+  // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
+  // address is chosen once; the other items' addresses are lds0/lds1 plus constants.
+  static_assert(ITEMS * RPP - HS < RPP, "scratch rows only in the last item");
+  const int waddr_last = ((lt >> 3) + RPP * (ITEMS - 1)) < HS ? item_lds(ITEMS - 1) : dump;
+  auto waddr = [&](int j) { return j == ITEMS - 1 ? waddr_last : item_lds(j); };
+  int inm = 0;  // bit j: item j's row is real input (or scratch) -- else zero padding
+  auto geometry_emit = [&](int k) __attribute__((always_inline)) {
+    int img0, y0;
+    tile_y0img(k, img0, y0);
+    int ltv = lt;
+    asm volatile("" : "+v"(ltv));
+    inm = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int r = (ltv >> 3) + RPP * j;
+      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+      const bool in = r >= HS || (iy >= 0 && iy < H && ix >= 0 && ix < W);
+      inm |= (int)in << j;
     }
   };
-  // stage p's item loads: buffer loads (32-bit byte offset into src1, or src2 = the concatenated
-  // skip input; the chunk's channel offset in soffset); past the last stage a zero-record
-  // descriptor, so every reload is unconditional (a conditional one keeps the old value alive
-  // beside the new one: a second register set the compiler rotates with waiting copies)
+  // stage loads: buffer loads (32-bit byte offset into src1, or src2 = the concatenated skip
+  // input; the chunk's channel offset in soffset); past the last stage a zero-record descriptor,
+  // so every reload is unconditional (a conditional one keeps the old value alive beside the new
+  // one: a second register set the compiler rotates with waiting copies)
   const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
   const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
   struct Src {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t rowb, so;
   };
-  auto src_of = [&](int p) __attribute__((always_inline)) {  // scalar selects only (uniform)
-    const int k = p / ncc, ci0 = (p - k * ncc) * 64;
-    const bool s1 = ci0 < a.C1, live = p < nstages;
+  auto src_of = [&](int cc, bool live) __attribute__((always_inline)) {  // scalar selects only (uniform)
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
     Src c;
     c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0,
                                              live ? (s1 ? nrec1 : nrec2) : 0, 0x00020000);
     c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
     c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
     return c;
-  };
-  auto coef_of = [&](int p) __attribute__((always_inline)) {
-    const int pp = p < nstages ? p : nstages - 1;
-    const int k = pp / ncc, cc = pp - k * ncc;
-    const int img = tile_p(k) / (H * W) + sg;
-    return (const f32x4*)(a.gn_coef + ((size_t)img * (Cin / 8) + cc * 8 + lch) * 16);
   };
   auto stage_addv = [&](int k) {
     const int tileP = tile_p(k), tileC = tile_c(k), img0 = tileP / (H * W);
@@ -2508,68 +2572,72 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
   };
   u32x4 h[ITEMS];
   f32x4 c[4], cn[4];
-  // transform stage p (items in h, coefficients in c) into hbuf; each item's register is reloaded
-  // with stage p+1's item right after its transform, stage p+1's coefficients go to cn first
-  // (older than every item reload: waiting for them never waits for an item). The masks are
-  // tile(p)'s; the reloads use tile(p+1)'s geometry.
-  auto emit = [&](int p, char* hbuf) __attribute__((always_inline)) {
-    const uint32_t okm = okmL, padm = padmL;
-    const int kn = (p + 1) / ncc;
-    if (p + 1 < nstages && kn != p / ncc) geometry(kn);
-    const f32x4* cp = coef_of(p + 1);
+  auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) c[q][e] = cn[q][e] * GN_L2E;
+  };
+  // the stage being loaded: tile kL, chunk ccL (the emitted stage is the one before it)
+  int kL = 0, ccL = 0;
+  // transform the emitted stage (items in h, coefficients in c) into hbuf; each item's register
+  // is reloaded with the loaded stage's item right after its transform; that stage's
+  // coefficients go to cn first (older than every item reload: waiting for them never waits for
+  // an item).
+  auto emit = [&](char* hbuf) __attribute__((always_inline)) {
+    if (ccL == 0) geometry_emit(kL);  // the emitted stage opens tile kL
+    if (++ccL == ncc) {
+      ccL = 0;
+      if (++kL < ntiles) geometry_pix(kL);
+    }
+    const bool live = kL < ntiles;
+    const f32x4* cp = (const f32x4*)(cbase + (live ? ccL : 0) * 128);
 #pragma unroll
     for (int q = 0; q < 4; ++q) cn[q] = cp[q];
-    const Src nx = src_of(p + 1);
+    const Src nx = src_of(ccL, live);
     typedef __attribute__((ext_vector_type(2))) float f32x2;
     typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      u32x4 y;
+      const uint32_t zm = (uint32_t)__builtin_amdgcn_sbfe(inm, j, 1);  // 0 (padding) or ~0
+      uint32_t yw[4];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint32_t xw = h[j][w];
-        const int e = 2 * (w & 1);
-        const float s0 = gn_silu_l2(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
-        const float s1 = gn_silu_l2(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
-        y[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{s0, s1}, bf16x2_t));
-      }
-      const bool ok = (okm >> j) & 1, keep = ok || ((padm >> j) & 1);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = ok ? y[e] : 0u;
-      *(u32x4*)(hbuf + (keep ? item_lds(j) : dump)) = y;
+      for (int hf = 0; hf < 2; ++hf)  // channels 4hf .. 4hf+3: words 2hf, 2hf+1
+        gn_silu_x4(h[j][2 * hf], h[j][2 * hf + 1], c[hf][0], c[hf][1], c[hf][2], c[hf][3], c[2 + hf][0],
+                   c[2 + hf][1], c[2 + hf][2], c[2 + hf][3], zm, yw[2 * hf], yw[2 * hf + 1]);
+      const u32x4 y = {yw[0], yw[1], yw[2], yw[3]};
+      *(u32x4*)(hbuf + waddr(j)) = y;
       __builtin_amdgcn_sched_barrier(0);
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(nx.rs, __umul24((uint32_t)ipix[j], nx.rowb) + lch * 16, nx.so, 0);
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = cn[q] * GN_L2E;  // prescaled: gn_silu_l2
+    prescale();
   };
   // prologue: stage 0 (and tile 0's addv)
-  geometry(0);
+  geometry_pix(0);
   {
-    const f32x4* cp = coef_of(0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = cp[q] * GN_L2E;
-    const Src s0 = src_of(0);
+    for (int q = 0; q < 4; ++q) cn[q] = ((const f32x4*)cbase)[q];
+    prescale();
+    const Src s0 = src_of(0, true);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(s0.rs, __umul24((uint32_t)ipix[j], s0.rowb) + lch * 16, s0.so, 0);
   }
   stage_addv(0);
-  emit(0, smem);
+  emit(smem);
 #ifdef ITSD_STAMPS
   st[5] = stamp() - t_begin;
 #endif
   block_sync();  // B0
-  for (int q = 0; q < nstages; ++q) {  // during MFMA stage q
-    const int k = q / ncc, cc = q - k * ncc;
+  for (int q = 0, k = 0, cc = 0; q < nstages; ++q) {  // during MFMA stage q = (tile k, chunk cc)
     STAMP(h0);
     // tile k's residual, during its last chunk (issued before the item reloads: the wait below
     // for it leaves them in flight); tile k+1's addv with its first chunk
     const bool res = RES && a.resid && cc == ncc - 1;
     if (res) res_dma(k);
     if (q + 1 < nstages) {
-      if ((q + 1) % ncc == 0) stage_addv((q + 1) / ncc);
-      emit(q + 1, smem + ((q + 1) & 1) * HALO);
+      if (cc == ncc - 1) stage_addv(k + 1);
+      emit(smem + ((q + 1) & 1) * HALO);
     }
     // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
     // issued after it, may still be in flight)
@@ -2580,6 +2648,10 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
     STAMP(h1);
     STAMP_ADD(3, h1 - h0);
     block_sync();  // end of MFMA stage q
+    if (++cc == ncc) {
+      cc = 0;
+      ++k;
+    }
   }
   PWS_STAMP_OUT();
 }
