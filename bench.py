@@ -4,18 +4,31 @@ One "step" = one RandomSearch round: N_local candidates per GPU x T=1000 DDPM st
 of the CIFAR-10 32x32 UNet (Arch A, config/config.yaml:25-29) in bf16 on MI355X,
 the Oracle verifier on every candidate, one all_gather of the scores, argmax.
 Weights: the seeded non-degenerate synthetic recipe (no checkpoint offline);
-noise: Philox. Weak scaling: every GPU owns N_local candidates.
+noise: Philox. Weak scaling by default (every GPU owns N_local candidates);
+--n-total N fixes the global N instead (strong scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-total N] [--no-extras]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
-Rank 0 prints ONE JSON line. Extra fields: roofline (conv kernel census with HIP
-events, same run) and cpu_baseline (the CPU oracle timed on this host's cores).
+Rank 0 prints ONE JSON line. Extra fields (single-GPU runs):
+  roofline      the dominant kernel (fused GroupNorm conv) in steady state with HIP events on
+                the UNet's stream, its PMC HBM traffic (profiles/, this commit), the conv tiles'
+                HBM GB/s, and the attention kernels' MFMA utilisation;
+  sweep         N in {64, 1024} (north_star), same path;
+  fp32          the reference-precision (parity mode) throughput at the headline N;
+  legs          the other BASELINE configs per GPU shard: C3 CFG zero-order round (Arch C,
+                N_local = 32 -> 2N = 64 guided batch), C4 64x64 Arch A (N_local = 16), C5
+                T = 3000 path search (N_local = 128), each with its own dominant kernel;
+  cpu_baseline  the CPU oracle (fp32) timed on this host's cores at B in {1, 8, 32} plus a
+                short full-loop conversion check.
+Windowed lines time a contiguous window of sampler steps (every DDPM step runs the same
+UNet, so candidate-images/s at T = N / (T x per-step time)); the window is stated in each.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -28,12 +41,22 @@ import torch.distributed as dist
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md, chip-level table)
 MFMA_FP32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBPS = 8000.0
+CONV_KINDS = ("conv", "convgn", "convgnw", "convgnw4")
+KERNEL_NAMES = {
+    "convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3, 128x128 tile)",
+    "convgnw": "conv3x3_gn_pws_kernel (persistent fused GroupNorm+SiLU+conv3x3, 128x256 tiles, W=32/16)",
+    "convgnw4": "conv3x3_gn_pws_kernel<8> (persistent fused GroupNorm+SiLU+conv3x3, 8x8 level)",
+    "conv": "conv_pipe / conv_small (implicit-GEMM conv)",
+    "attn": "attn_mfma_kernel / attn_flash_kernel (self-attention on MFMA)",
+}
 
 
-def cpu_baseline(T: int, seconds: float = 15.0, batch: int = 8):
-    """Reference-equivalent CPU sampler (oracle, fp32) on this host's cores: UNet
-    forwards of Arch A at batch `batch` for ~`seconds`, converted to candidate-images/s
-    at T steps (img-fwd/s / T; the sampler update is negligible next to the forward)."""
+def cpu_baseline(T: int, seconds: float = 15.0):
+    """Reference-equivalent CPU sampler (oracle, fp32) on this host's cores: UNet forwards of
+    Arch A at B in {1, 8, 32} (about seconds/3 each), converted to candidate-images/s at T
+    (img-fwd/s / T; the sampler update is negligible next to the forward), plus one full
+    N = 1 p_sample loop over a short T (the conversion check)."""
     from oracle import ref_cpu as R
     from itsd.arch import ARCH_A
     from itsd.weights import synthetic_state_dict
@@ -43,23 +66,149 @@ def cpu_baseline(T: int, seconds: float = 15.0, batch: int = 8):
     torch.set_num_threads(cores)
     a = ARCH_A
     sd = synthetic_state_dict(a, 0)
-    x = torch.randn(batch, 3, 32, 32)
-    t = torch.full((batch,), 500, dtype=torch.long)
+    fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
     sch = R.schedule(1e-4, 0.02, T)
+    per_b = {}
     with torch.no_grad():
-        fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
-        R.p_sample_loop(fw, x, sch, lambda s, xx: torch.randn_like(xx), t_begin=T - 1, t_end=T - 1, clip=False)
-        n = 0
+        for b in (1, 8, 32):
+            x = torch.randn(b, 3, 32, 32)
+            t = torch.full((b,), 500, dtype=torch.long)
+            fw(x, t)  # warm
+            n, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds / 3 or n == 0:
+                fw(x, t)
+                n += 1
+            dt = time.perf_counter() - t0
+            per_b[b] = n * b / dt
+        # conversion check: a full N = 1 ancestral loop over Tc steps
+        Tc = 20
+        sc = R.schedule(1e-4, 0.02, Tc)
+        x = torch.randn(1, 3, 32, 32)
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
-            step = T - 1 - (n % (T - 1))
-            x = R.p_sample_loop(fw, x, sch, lambda s, xx: torch.randn_like(xx), t_begin=step, t_end=step, clip=False)
-            n += 1
+        R.p_sample_loop(fw, x, sc, lambda s, xx: torch.randn_like(xx))
+        dtc = time.perf_counter() - t0
+    best_b = max(per_b, key=per_b.get)
+    return {"value": per_b[best_b] / T, "unit": "candidate-images/sec", "cores": cores, "kind": "port",
+            "sample": f"Arch A fp32 UNet forwards at B=1/8/32: {per_b[1]:.2f}/{per_b[8]:.2f}/{per_b[32]:.2f} "
+                      f"img-fwd/s ({seconds / 3:.0f}s each), value = best (B={best_b}) / T={T}; "
+                      f"check: full N=1 loop of {Tc} steps {dtc:.2f}s = {Tc / dtc:.2f} steps/s vs "
+                      f"{per_b[1]:.2f} img-fwd/s at B=1",
+            "img_fwd_per_s": {str(k): round(v, 3) for k, v in per_b.items()},
+            "full_loop_check": {"T": Tc, "N": 1, "seconds": round(dtc, 3), "steps_per_s": round(Tc / dtc, 3)}}
+
+
+def census(net, n: int, img: int, labels=None):
+    """Per-launch census of one forward (HIP events on the UNet's stream): per kind
+    [launches, ms, flops] and the op list."""
+    dev = net.device
+    x = torch.randn(n, 3, img, img, device=dev)
+    t = torch.full((n,), 500, dtype=torch.int32, device=dev)
+    nat = net.native(n)
+    for _ in range(2):
+        ops = nat.profile_ops(x, t)
+    agg = {}
+    for o in ops:
+        g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
+        g[0] += 1
+        g[1] += o["ms"]
+        g[2] += o["flops"]
+    return ops, agg, nat, x, t
+
+
+def conv_alg_bytes(o) -> float:
+    """Algorithmic HBM bytes of one bf16 conv launch: input activations once, weights once,
+    output once (the GroupNorm statistics and bias rows are negligible)."""
+    ks = max(1, o["ks"])
+    cin = o["K"] // (ks * ks)
+    su = o["stride_up"]
+    stride, ups = su // 10, su % 10
+    m_in = o["M"] * stride * stride if not ups else o["M"] // 4
+    return 2.0 * (m_in * cin + o["N"] * o["K"] + o["M"] * o["N"])
+
+
+def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
+    conv = {k: v for k, v in agg.items() if k in CONV_KINDS}
+    kind = max(conv, key=lambda k: conv[k][1])
+    n_l, ms_census, fl_sum = conv[kind]
+    if steady:
+        # each launch replayed 10x back to back between HIP events (itsd_profile_op): what the
+        # replayed step graph sees, without the eager census's per-launch event overhead
+        ms_sum = sum(nat.profile_op(x, t, i, reps=10) for i, o in enumerate(ops) if o["kind"] == kind)
+    else:
+        ms_sum = ms_census
+    achieved = fl_sum / (ms_sum * 1e-3) / 1e12
+    peak = MFMA_BF16_PEAK_TFLOPS if precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
+    return kind, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                  "frac": round(achieved / peak, 4), "kernel": KERNEL_NAMES[kind], "launches_per_forward": n_l,
+                  "avg_launch_ms": round(ms_sum / n_l, 4), "census_avg_launch_ms": round(ms_census / n_l, 4),
+                  "flops_per_launch": fl_sum / n_l}
+
+
+def windowed_rate(smp, n: int, img: int, T: int, window: int, labels=None, rounds: int = 1):
+    """Candidate-images/s at T from a timed window of `window` sampler steps (t = T-1 ..)."""
+    dev = smp.model.device
+    x = torch.randn(n, 3, img, img, device=dev)
+    lab = labels
+    smp.run(x, t_begin=T - 1, t_end=T - window, labels=lab, seed=7, clip=False)  # capture + warm
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(rounds):
+        x = torch.randn(n, 3, img, img, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        smp.run(x, t_begin=T - 1, t_end=T - window, labels=lab, seed=11, clip=False)
+        torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-    img_fwd_s = n * batch / dt
-    return {"value": img_fwd_s / T, "unit": "candidate-images/sec", "cores": cores, "kind": "port",
-            "sample": f"{n} sampler steps of Arch A fp32 at batch {batch} ({dt:.1f}s, {img_fwd_s:.2f} img-fwd/s), "
-                      f"converted at T={T}"}
+        best = dt if best is None else min(best, dt)
+    ms_step = best / window * 1e3
+    return n / (T * ms_step * 1e-3), ms_step
+
+
+def leg(name, make_net, n: int, img: int, T: int, window: int, cfg: bool, precision: str = "bf16",
+        workload: str = ""):
+    from itsd.diffusion import CondGaussianDiffusionSampler, GaussianDiffusionSampler
+
+    net = make_net()
+    net.reserve(2 * n if cfg else n)
+    if cfg:
+        smp = CondGaussianDiffusionSampler(net, 1e-4, 0.028, T, w=1.8)
+        labels = (torch.arange(n, device=net.device) % 10 + 1).to(torch.int32)
+    else:
+        smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
+        labels = None
+    rate, ms_step = windowed_rate(smp, n, img, T, window, labels)
+    out = {"workload": workload, "value": round(rate, 4), "unit": "candidate-images/sec per GPU",
+           "ms_per_step": round(ms_step, 3), "T": T, "N_local": n, "dtype": precision,
+           "sample": f"steps t={T - 1}..{T - window} ({window} of {T}) timed, converted to T={T}"}
+    try:
+        bn = 2 * n if cfg else n
+        ops, agg, nat, x, t = census(net, bn, img) if not cfg else _cfg_census(net, bn, img)
+        kind, roof = dominant_roofline(ops, agg, nat, x, t, precision, steady=not cfg)
+        out["roofline"] = roof
+    except Exception as e:  # the leg's number stands without its census
+        out["roofline_error"] = repr(e)
+    del smp, net
+    torch.cuda.empty_cache()
+    return out
+
+
+def _cfg_census(net, n: int, img: int):
+    """Census of the CFG UNet (labels needed): the guided step's 2N forward."""
+    dev = net.device
+    x = torch.randn(n, 3, img, img, device=dev)
+    t = torch.full((n,), 500, dtype=torch.int32, device=dev)
+    nat = net.native(n)
+    # profile_ops passes no labels: the CFG forward reads label 0 (the unconditional row) --
+    # the same launches, shapes and FLOPs as the guided batch
+    for _ in range(2):
+        ops = nat.profile_ops(x, t)
+    agg = {}
+    for o in ops:
+        g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
+        g[0] += 1
+        g[1] += o["ms"]
+        g[2] += o["flops"]
+    return ops, agg, nat, x, t
 
 
 def main():
@@ -68,10 +217,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n-per-gpu", type=int, default=256)
+    ap.add_argument("--n-total", type=int, default=0, help="strong scaling: fixed global N split over the GPUs")
     ap.add_argument("--T", type=int, default=1000)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip sweep / fp32 / legs")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -84,15 +235,20 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import itsd
-    from itsd.arch import ARCH_A, flops_per_image
+    from itsd.arch import ARCH_A, ARCH_C, flops_per_image
     from itsd.diffusion import GaussianDiffusionSampler
-    from itsd.model import UNet
+    from itsd.model import CondUNet, UNet
     from itsd.search import SearchEngine
     from itsd.verifier import OracleVerifier
 
     a = ARCH_A
-    n_local = args.n_per_gpu
-    n_total = n_local * world
+    if args.n_total:
+        if args.n_total % world:
+            raise SystemExit(f"--n-total {args.n_total} does not split over {world} GPUs")
+        n_total, n_local, scaling = args.n_total, args.n_total // world, "strong"
+    else:
+        n_local, scaling = args.n_per_gpu, "weak"
+        n_total = n_local * world
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision=args.precision,
                weights="gauss", seed=0, device=dev)
     smp = GaussianDiffusionSampler(net, 1e-4, 0.02, args.T)
@@ -119,56 +275,86 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    # Roofline of the dominant kernel: one census forward at the bench batch with HIP events
-    # around every launch on the UNet's stream (itsd_profile_ops) picks the conv kind with the
-    # most time ("convgnw" = conv3x3_gn_wide_kernel<1>, "convgnw4" = <4>, "convgn" =
-    # conv3x3_gn_kernel, "conv" = the plain conv kernels); its launches are then timed in steady
-    # state (itsd_profile_op). FLOPs are the MFMA work each launch executes.
     roof = None
     if rank == 0:
-        x = torch.randn(n_local, 3, 32, 32, device=dev)
-        t = torch.full((n_local,), 500, dtype=torch.int32, device=dev)
-        nat = net.native(n_local)
-        for _ in range(2):
-            ops = nat.profile_ops(x, t)
-        agg = {}
-        for o in ops:
-            if o["kind"] in ("conv", "convgn", "convgnw", "convgnw4"):
-                g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
-                g[0] += 1
-                g[1] += o["ms"]
-                g[2] += o["flops"]
-        kind = max(agg, key=lambda k: agg[k][1])
-        n_l, ms_census, fl_sum = agg[kind]
-        # per-launch time of the dominant kernel in steady state: each of its launches replayed
-        # 10x back to back between HIP events on the UNet's stream (itsd_profile_op) -- what
-        # the replayed step graph sees, without the eager census's per-launch event overhead
-        ms_sum = sum(nat.profile_op(x, t, i, reps=10) for i, o in enumerate(ops) if o["kind"] == kind)
-        avg_ms = ms_sum / n_l
-        achieved = fl_sum / (ms_sum * 1e-3) / 1e12
-        peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
+        ops, agg, nat, x, t = census(net, n_local, 32)
+        kind, roof = dominant_roofline(ops, agg, nat, x, t, args.precision)
+        n_l = roof["launches_per_forward"]
         total_ms = sum(o["ms"] for o in ops)
-        conv_ms = sum(v[1] for v in agg.values())
-        conv_fl = sum(v[2] for v in agg.values())
-        names = {"convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3, 128x128 tile)",
-                 "convgnw": "conv3x3_gn_wide_kernel<1> (fused GroupNorm+SiLU+conv3x3, 128x256 tile)",
-                 "convgnw4": "conv3x3_gn_wide_kernel<4> (fused GroupNorm+SiLU+conv3x3, 8x8 level)",
-                 "conv": "conv_pipe_wide / conv_pipe / conv_small (implicit-GEMM conv)"}
+        conv_ms = sum(v[1] for k, v in agg.items() if k in CONV_KINDS)
+        conv_fl = sum(v[2] for k, v in agg.items() if k in CONV_KINDS)
+        # HBM traffic of the dominant kernel: PMC passes of this commit (tools/pmc_passes.sh at
+        # N = 256, corrected as MI355X_MICROARCH.md prescribes), per launch
         traffic = None
         tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kind}.json")
         if os.path.exists(tfile) and args.precision == "bf16" and n_local == 256:
             with open(tfile) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": names[kind], "launches_per_forward": n_l, "avg_launch_ms": round(avg_ms, 4),
-                "census_avg_launch_ms": round(ms_census / n_l, 4),
-                "flops_per_launch": fl_sum / n_l,
-                "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
-                "all_conv_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
-                "conv_share_of_forward": round(conv_ms / total_ms, 4),
-                "forward_ms": round(total_ms, 3),
-                "forward_tflops_algorithmic": round(flops_per_image(a) * n_local / (total_ms * 1e-3) / 1e12, 2)}
+        dom = [o for o in ops if o["kind"] == kind]
+        alg_b = sum(conv_alg_bytes(o) for o in dom) / len(dom)
+        avg_s = roof["avg_launch_ms"] * 1e-3
+        roof.update({
+            "traffic": traffic,
+            "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
+            "all_conv_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+            "conv_share_of_forward": round(conv_ms / total_ms, 4),
+            "forward_ms": round(total_ms, 3),
+            "forward_tflops_algorithmic": round(flops_per_image(a) * n_local / (total_ms * 1e-3) / 1e12, 2),
+            # north_star: HBM GB/s of the conv tiles (dominant kernel) against the 8 TB/s peak
+            "conv_hbm": {"kernel": KERNEL_NAMES[kind], "alg_bytes_per_launch": alg_b,
+                         "alg_gbps": round(alg_b / avg_s / 1e9, 1),
+                         "pmc_bytes_per_launch": traffic,
+                         "pmc_gbps": round(traffic / avg_s / 1e9, 1) if traffic else None,
+                         "pmc_frac_of_peak": round(traffic / avg_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
+                         "peak_gbps": HBM_PEAK_GBPS},
+        })
+        if "attn" in agg:
+            al, ams, afl = agg["attn"]
+            at = afl / (ams * 1e-3) / 1e12
+            roof["attention"] = {"kernel": KERNEL_NAMES["attn"], "launches_per_forward": al,
+                                 "avg_launch_ms": round(ams / al, 4), "tflops": round(at, 2),
+                                 "mfma_frac": round(at / MFMA_BF16_PEAK_TFLOPS, 4),
+                                 "share_of_forward": round(ams / total_ms, 4)}
+
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras:
+        # north_star N sweep on the same path (headline N is the main line)
+        sweep = {}
+        for n, window in ((64, 1000), (1024, 100)):
+            if n == n_local:
+                continue
+            net.reserve(n)
+            rate, ms = windowed_rate(smp, n, 32, args.T, window)
+            sweep[str(n)] = {"value": round(rate, 3), "ms_per_step": round(ms, 3),
+                             "sample": f"{window} of {args.T} steps timed"}
+        sweep[str(n_local)] = {"value": round(n_total * args.steps / dt, 3), "ms_per_step":
+                               round(dt / args.steps / args.T * 1e3, 3), "sample": "headline"}
+        extras["sweep"] = {"unit": "candidate-images/sec", "T": args.T, "dtype": args.precision, "points": sweep}
+        del eng, smp, net, nat
+        torch.cuda.empty_cache()
+        if args.precision == "bf16":
+            extras["fp32"] = leg("fp32", lambda: UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0,
+                                                      img_size=32, precision="fp32", weights="gauss", seed=0,
+                                                      device=dev),
+                                 n_local, 32, args.T, 20, cfg=False, precision="fp32",
+                                 workload=f"Arch A 32 px, N={n_local}, fp32 parity mode (the reference's precision)")
+        c = ARCH_C
+        extras["legs"] = {
+            "C3": leg("C3", lambda: CondUNet(c.T, c.num_labels, c.ch, c.ch_mult, c.num_res_blocks, 0.0, img_size=32,
+                                             precision="bf16", weights="gauss", seed=0, device=dev),
+                      32, 32, 1000, 50, cfg=True,
+                      workload="CFG zero-order round per GPU shard: Arch C (MainCondition.py), N_local=32 "
+                               "(2N=64 guided batch), T=1000, w=1.8"),
+            "C4": leg("C4", lambda: UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=64,
+                                         precision="bf16", weights="gauss", seed=0, device=dev),
+                      16, 64, 1000, 50, cfg=False,
+                      workload="64x64 Arch A per GPU shard (N=128 over 8 GPUs): N_local=16, T=1000"),
+            "C5": leg("C5", lambda: UNet(3000, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32,
+                                         precision="bf16", weights="gauss", seed=0, device=dev),
+                      128, 32, 3000, 100, cfg=False,
+                      workload="T=3000 path search per GPU shard (N=1024 over 8 GPUs): N_local=128, "
+                               "fine_tune_extended_T.py schedule"),
+        }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -180,7 +366,7 @@ def main():
             "metric": "candidate-images/sec at T=1000, CIFAR-10 32x32 UNet, N=256, 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "candidate-images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": scaling, "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (Philox noise, seeded non-degenerate random-init weights)",
             "config": {"workload": f"random-search round: N={n_local}/GPU candidates x T={args.T} DDPM steps, "
                                    f"Arch A UNet 32x32 (ch128 [1,2,3,4] attn[2] nrb2), Oracle verifier",
@@ -189,6 +375,7 @@ def main():
                        "best_candidate": best},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        out.update(extras)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
