@@ -43,12 +43,12 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md, chip-l
 MFMA_FP32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBPS = 8000.0
 CONV_KINDS = ("conv", "convgn", "convgnw", "convgnw4")
-KERNEL_NAMES = {
-    "convgn": "conv3x3_gn_kernel (fused GroupNorm+SiLU+conv3x3, 128x128 tile)",
-    "convgnw": "conv3x3_gn_pws_kernel (persistent fused GroupNorm+SiLU+conv3x3, 128x256 tiles, W=32/16)",
-    "convgnw4": "conv3x3_gn_pws_kernel<8> (persistent fused GroupNorm+SiLU+conv3x3, 8x8 level)",
-    "conv": "conv_pipe / conv_small (implicit-GEMM conv)",
-    "attn": "attn_mfma_kernel / attn_flash_kernel (self-attention on MFMA)",
+KERNEL_NAMES = {  # op classes of the census
+    "convgn": "fused GroupNorm+SiLU+conv3x3, 128-pixel tiles",
+    "convgnw": "fused GroupNorm+SiLU+conv3x3, 256-pixel tiles (32x32 / 16x16 levels)",
+    "convgnw4": "fused GroupNorm+SiLU+conv3x3, 256-pixel tiles of four 8x8 images",
+    "conv": "implicit-GEMM conv (1x1, strided, sub-pixel upsample, 4x4 level)",
+    "attn": "self-attention on MFMA",
 }
 
 
@@ -126,22 +126,41 @@ def conv_alg_bytes(o) -> float:
     return 2.0 * (m_in * cin + o["N"] * o["K"] + o["M"] * o["N"])
 
 
+def rocprof_name(kernel: str) -> str:
+    """The census kernel name (the ITSD_LAUNCH expression) as rocprofv3 prints it (bf16 builds)."""
+    k = kernel.strip("()").replace("<T,", "<unsigned short,").replace("<T>", "<unsigned short>")
+    return k
+
+
+def kernel_file(kernel: str) -> str:
+    return "".join(ch if ch.isalnum() else "_" for ch in rocprof_name(kernel)).strip("_")
+
+
 def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
-    conv = {k: v for k, v in agg.items() if k in CONV_KINDS}
-    kind = max(conv, key=lambda k: conv[k][1])
-    n_l, ms_census, fl_sum = conv[kind]
+    """Roofline of the conv kernel FUNCTION with the most time in the census forward."""
+    per = {}
+    for i, o in enumerate(ops):
+        if o["kind"] in CONV_KINDS:
+            g = per.setdefault(o["kernel"] or o["kind"], [0, 0.0, 0.0, [], o["kind"]])
+            g[0] += 1
+            g[1] += o["ms"]
+            g[2] += o["flops"]
+            g[3].append(i)
+    kernel = max(per, key=lambda k: per[k][1])
+    n_l, ms_census, fl_sum, idx, kind = per[kernel]
     if steady:
         # each launch replayed 10x back to back between HIP events (itsd_profile_op): what the
         # replayed step graph sees, without the eager census's per-launch event overhead
-        ms_sum = sum(nat.profile_op(x, t, i, reps=10) for i, o in enumerate(ops) if o["kind"] == kind)
+        ms_sum = sum(nat.profile_op(x, t, i, reps=10) for i in idx)
     else:
         ms_sum = ms_census
     achieved = fl_sum / (ms_sum * 1e-3) / 1e12
     peak = MFMA_BF16_PEAK_TFLOPS if precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
-    return kind, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                  "frac": round(achieved / peak, 4), "kernel": KERNEL_NAMES[kind], "launches_per_forward": n_l,
-                  "avg_launch_ms": round(ms_sum / n_l, 4), "census_avg_launch_ms": round(ms_census / n_l, 4),
-                  "flops_per_launch": fl_sum / n_l}
+    return kernel, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "kernel": rocprof_name(kernel),
+                    "family": KERNEL_NAMES[kind], "launches_per_forward": n_l,
+                    "avg_launch_ms": round(ms_sum / n_l, 4), "census_avg_launch_ms": round(ms_census / n_l, 4),
+                    "flops_per_launch": fl_sum / n_l}
 
 
 def windowed_rate(smp, n: int, img: int, T: int, window: int, labels=None, rounds: int = 1):
@@ -182,33 +201,14 @@ def leg(name, make_net, n: int, img: int, T: int, window: int, cfg: bool, precis
            "sample": f"steps t={T - 1}..{T - window} ({window} of {T}) timed, converted to T={T}"}
     try:
         bn = 2 * n if cfg else n
-        ops, agg, nat, x, t = census(net, bn, img) if not cfg else _cfg_census(net, bn, img)
-        kind, roof = dominant_roofline(ops, agg, nat, x, t, precision, steady=not cfg)
+        ops, agg, nat, x, t = census(net, bn, img)
+        _, roof = dominant_roofline(ops, agg, nat, x, t, precision)
         out["roofline"] = roof
     except Exception as e:  # the leg's number stands without its census
         out["roofline_error"] = repr(e)
     del smp, net
     torch.cuda.empty_cache()
     return out
-
-
-def _cfg_census(net, n: int, img: int):
-    """Census of the CFG UNet (labels needed): the guided step's 2N forward."""
-    dev = net.device
-    x = torch.randn(n, 3, img, img, device=dev)
-    t = torch.full((n,), 500, dtype=torch.int32, device=dev)
-    nat = net.native(n)
-    # profile_ops passes no labels: the CFG forward reads label 0 (the unconditional row) --
-    # the same launches, shapes and FLOPs as the guided batch
-    for _ in range(2):
-        ops = nat.profile_ops(x, t)
-    agg = {}
-    for o in ops:
-        g = agg.setdefault(o["kind"], [0, 0.0, 0.0])
-        g[0] += 1
-        g[1] += o["ms"]
-        g[2] += o["flops"]
-    return ops, agg, nat, x, t
 
 
 def main():
@@ -278,7 +278,7 @@ def main():
     roof = None
     if rank == 0:
         ops, agg, nat, x, t = census(net, n_local, 32)
-        kind, roof = dominant_roofline(ops, agg, nat, x, t, args.precision)
+        kernel, roof = dominant_roofline(ops, agg, nat, x, t, args.precision)
         n_l = roof["launches_per_forward"]
         total_ms = sum(o["ms"] for o in ops)
         conv_ms = sum(v[1] for k, v in agg.items() if k in CONV_KINDS)
@@ -286,11 +286,11 @@ def main():
         # HBM traffic of the dominant kernel: PMC passes of this commit (tools/pmc_passes.sh at
         # N = 256, corrected as MI355X_MICROARCH.md prescribes), per launch
         traffic = None
-        tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kind}.json")
+        tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kernel_file(kernel)}.json")
         if os.path.exists(tfile) and args.precision == "bf16" and n_local == 256:
             with open(tfile) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
-        dom = [o for o in ops if o["kind"] == kind]
+        dom = [o for o in ops if (o["kernel"] or o["kind"]) == kernel]
         alg_b = sum(conv_alg_bytes(o) for o in dom) / len(dom)
         avg_s = roof["avg_launch_ms"] * 1e-3
         roof.update({
@@ -301,7 +301,7 @@ def main():
             "forward_ms": round(total_ms, 3),
             "forward_tflops_algorithmic": round(flops_per_image(a) * n_local / (total_ms * 1e-3) / 1e12, 2),
             # north_star: HBM GB/s of the conv tiles (dominant kernel) against the 8 TB/s peak
-            "conv_hbm": {"kernel": KERNEL_NAMES[kind], "alg_bytes_per_launch": alg_b,
+            "conv_hbm": {"kernel": rocprof_name(kernel), "alg_bytes_per_launch": alg_b,
                          "alg_gbps": round(alg_b / avg_s / 1e9, 1),
                          "pmc_bytes_per_launch": traffic,
                          "pmc_gbps": round(traffic / avg_s / 1e9, 1) if traffic else None,
@@ -311,7 +311,8 @@ def main():
         if "attn" in agg:
             al, ams, afl = agg["attn"]
             at = afl / (ams * 1e-3) / 1e12
-            roof["attention"] = {"kernel": KERNEL_NAMES["attn"], "launches_per_forward": al,
+            akern = sorted({rocprof_name(o["kernel"]) for o in ops if o["kind"] == "attn"})
+            roof["attention"] = {"kernel": " / ".join(akern), "launches_per_forward": al,
                                  "avg_launch_ms": round(ams / al, 4), "tflops": round(at, 2),
                                  "mfma_frac": round(at / MFMA_BF16_PEAK_TFLOPS, 4),
                                  "share_of_forward": round(ams / total_ms, 4)}

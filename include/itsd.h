@@ -135,9 +135,12 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
                          double* conv_flops, int* conv_launches, double* total_ms, void* stream);
 
 /* Per-launch census of one forward (synchronous, eager, HIP events): for launch i
- * (head, program ops in order, tail GN, tail) kinds[i] (0 GN, 1 conv, 2 attention,
- * -1 head, -2 tail), ms[i], flops[i] and shapes[6*i..] = {M, Cout, K or Cin, Hout,
- * ksize, 10*stride+upsample}. At most max_ops entries; *n_ops = entries written. */
+ * (head, program ops in order, tail GN, tail) kinds[i] = (kernel << 8) | (kind & 0xff) with
+ * kind the op class (0 GN, 1 conv, 2 attention, 3 GN finalize, 4/5/6 fused GroupNorm conv
+ * 128 px / 256 px / 8x8 level; -1 head, -2 tail, as a signed byte) and kernel the id of
+ * the first kernel the launch ran (itsd_kernel_name), ms[i], flops[i] and shapes[6*i..] =
+ * {M, Cout, K or Cin, Hout, ksize, 10*stride+upsample}. CFG UNets run with label 0.
+ * At most max_ops entries; *n_ops = entries written. */
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
                      double* ms, double* flops, int* shapes, int* n_ops, void* stream);
 
@@ -158,6 +161,10 @@ int itsd_set_option(const char* key, int value);
  * instantiated so far; a search replays one graph across all its rounds), "max_batch",
  * "T_sched", "ws_bytes" (activation arena), "ops" (program length). */
 int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value);
+
+/* Name of census kernel id `id` (itsd_profile_ops): the launch site's kernel expression,
+ * e.g. "conv3x3_gn_pws_kernel<32>"; "" for 0 / unknown ids. */
+const char* itsd_kernel_name(int id);
 
 const char* itsd_last_error(void);
 int itsd_version(void);

@@ -645,6 +645,7 @@ struct RunCtx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>>* evs = nullptr;
   std::vector<int>* ev_kind = nullptr;
   std::vector<double>* ev_flops = nullptr;
+  std::vector<int>* ev_kid = nullptr;  // kernel_id of the op's first launch (itsd_kernel_name)
 };
 
 int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
@@ -764,11 +765,13 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, s));
+    itsd::g_last_kernel = nullptr;
     int r = fn();
     HIPCHK(hipEventRecord(b, s));
     c.evs->push_back({a, b});
     c.ev_kind->push_back(kind);
     c.ev_flops->push_back(fl);
+    if (c.ev_kid) c.ev_kid->push_back(itsd::kernel_id(itsd::g_last_kernel));
     return r;
   };
   // head
@@ -881,9 +884,31 @@ int check_batch(itsd_unet* u, int n) {
 }  // namespace
 
 // ============================================================================ C ABI
+namespace itsd {
+const char* g_last_kernel = nullptr;
+std::vector<const char*>& kernel_names() {
+  static std::vector<const char*> v;
+  return v;
+}
+// ids of launch-site names: 0 = none recorded, else 1 + index in kernel_names() (the names are
+// the ITSD_LAUNCH string literals, so equal sites compare equal by content)
+int kernel_id(const char* name) {
+  if (!name) return 0;
+  auto& v = kernel_names();
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i] == name || !std::strcmp(v[i], name)) return (int)i + 1;
+  v.push_back(name);
+  return (int)v.size();
+}
+}  // namespace itsd
+
 extern "C" {
 
 int itsd_version(void) { return 1; }
+
+const char* itsd_kernel_name(int id) {
+  return id > 0 && id <= (int)itsd::kernel_names().size() ? itsd::kernel_names()[id - 1] : "";
+}
 
 int itsd_set_option(const char* key, int value) {
   if (!key) return fail(ITSD_ERR_INVALID, "null key");
@@ -1218,7 +1243,6 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
 int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int op_index, int reps, double* ms,
                     void* stream) {
   if (!u || !x || !t || !ms || reps < 1) return fail(ITSD_ERR_INVALID, "null argument or reps < 1");
-  if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_op: DDPM only");
   if (op_index < 1 || op_index > (int)u->ops.size()) return fail(ITSD_ERR_INVALID, "profile_op: op_index out of range");
   CHK(check_batch(u, n));
   HIPCHK(hipSetDevice(u->device));
@@ -1226,11 +1250,18 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   float* eps = nullptr;
   HIPCHK(hipMalloc(&eps, (size_t)n * 3 * u->H * u->H * 4));
+  // CFG: label 0 (the unconditional row) for every image -- the guided batch's launches, shapes
+  // and FLOPs
+  int32_t* lab0 = nullptr;
+  if (u->cfg) {
+    HIPCHK(hipMalloc(&lab0, (size_t)n * 4));
+    HIPCHK(hipMemsetAsync(lab0, 0, (size_t)n * 4, s));
+  }
   int r = temb_rows(u, t, n, 0, false, u->proj_buf, s);
   RunCtx c{};
   c.nb = n; c.x = x; c.x_mod = n;
   c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
-  c.label_mod = n; c.uncond_from = -1;
+  c.labels = lab0; c.label_mod = n; c.uncond_from = -1;
   c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
   if (r == ITSD_OK) r = run_program(u, c, s);  // every op's inputs in place
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1247,6 +1278,7 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
   hipFree(eps);
+  if (lab0) hipFree(lab0);
   CHK(r);
   HIPCHK(e);
   *ms = (double)m / reps;
@@ -1256,23 +1288,27 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds, double* ms,
                      double* flops, int* shapes, int* n_ops, void* stream) {
   if (!u || !x || !t || !n_ops) return fail(ITSD_ERR_INVALID, "null argument");
-  if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_ops: DDPM only");
   CHK(check_batch(u, n));
   HIPCHK(hipSetDevice(u->device));
   hipStream_t s = u->stream;
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   float* eps = nullptr;
   HIPCHK(hipMalloc(&eps, (size_t)n * 3 * u->H * u->H * 4));
+  int32_t* lab0 = nullptr;  // CFG: label 0 for every image (as itsd_profile_op)
+  if (u->cfg) {
+    HIPCHK(hipMalloc(&lab0, (size_t)n * 4));
+    HIPCHK(hipMemsetAsync(lab0, 0, (size_t)n * 4, s));
+  }
   CHK(temb_rows(u, t, n, 0, false, u->proj_buf, s));
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
-  std::vector<int> kd;
+  std::vector<int> kd, kid;
   std::vector<double> fl;
   RunCtx c{};
   c.nb = n; c.x = x; c.x_mod = n;
   c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
-  c.label_mod = n; c.uncond_from = -1;
+  c.labels = lab0; c.label_mod = n; c.uncond_from = -1;
   c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
-  c.census = true; c.evs = &evs; c.ev_kind = &kd; c.ev_flops = &fl;
+  c.census = true; c.evs = &evs; c.ev_kind = &kd; c.ev_flops = &fl; c.ev_kid = &kid;
   int r = run_program(u, c, s);
   hipError_t e = hipStreamSynchronize(s);
   // launch order: head, ops..., tail GN, tail
@@ -1283,7 +1319,7 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
     hipEventDestroy(evs[i].first);
     hipEventDestroy(evs[i].second);
     if (k >= max_ops) continue;
-    if (kinds) kinds[k] = kd[i];
+    if (kinds) kinds[k] = (kid[i] << 8) | (kd[i] & 0xff);
     if (ms) ms[k] = m;
     if (flops) flops[k] = fl[i];
     if (shapes) {
@@ -1305,6 +1341,7 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
   }
   *n_ops = k;
   hipFree(eps);
+  if (lab0) hipFree(lab0);
   CHK(r);
   HIPCHK(e);
   return ITSD_OK;

@@ -15,6 +15,16 @@ extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option
 extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
+// Census (itsd_profile_ops): the first kernel an op launches. Every launch site goes through
+// ITSD_LAUNCH, which records the kernel expression's name if none is recorded yet; the census
+// clears it before each op and maps the name to a small id (kernel_id, itsd_kernel_name).
+extern const char* g_last_kernel;
+int kernel_id(const char* name);
+#define ITSD_LAUNCH(K, ...)                                    \
+  do {                                                         \
+    if (!::itsd::g_last_kernel) ::itsd::g_last_kernel = #K;    \
+    hipLaunchKernelGGL(K, __VA_ARGS__);                        \
+  } while (0)
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
 

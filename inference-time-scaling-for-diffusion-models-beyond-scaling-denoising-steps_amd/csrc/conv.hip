@@ -2701,7 +2701,7 @@ __global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
 }
 
 hipError_t launch_gn_coef(const GNArgs& g, int n, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(gn_coef_kernel, dim3(n), dim3(256), 0, s, g, coef);
+  ITSD_LAUNCH(gn_coef_kernel, dim3(n), dim3(256), 0, s, g, coef);
   return hipGetLastError();
 }
 
@@ -2795,7 +2795,7 @@ hipError_t launch_head_mfma(const HeadArgs& h, hipStream_t s) {
   if (!h.wmf || (HW % 128 && 128 % HW) || (HW >= 128 && 128 % h.W) || h.Cout % 8 ||
       (size_t)(128 * 132 + nimg * 3 * (rows + 2) * (h.W + 2)) * 4 > (size_t)EPI_BYTES)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_mfma_kernel, dim3((unsigned)(((long long)h.n * HW + 127) / 128), (h.Cout + 127) / 128), dim3(256), 0,
+  ITSD_LAUNCH(head_mfma_kernel, dim3((unsigned)(((long long)h.n * HW + 127) / 128), (h.Cout + 127) / 128), dim3(256), 0,
                      s, h);
   return hipGetLastError();
 }
@@ -2846,10 +2846,10 @@ static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) 
   }
   if (g_conv_wide != 2 && blocks * S < 192) return false;
   grid.z = S;
-  hipLaunchKernelGGL(conv_pipe_wide, grid, dim3(512), 0, s, a);
+  ITSD_LAUNCH(conv_pipe_wide, grid, dim3(512), 0, s, a);
   *err = hipGetLastError();
   if (*err == hipSuccess && S > 1) {
-    hipLaunchKernelGGL(splitk_wide_epilogue_kernel, dim3(grid.x, grid.y), dim3(512), 0, s, a, S);
+    ITSD_LAUNCH(splitk_wide_epilogue_kernel, dim3(grid.x, grid.y), dim3(512), 0, s, a, S);
     *err = hipGetLastError();
   }
   return true;
@@ -2866,50 +2866,50 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           // persistent: one block per CU (160 KiB of LDS each), tiles strided over the grid
           const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
           const dim3 gp(std::min(tiles, g_num_cus));
-          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
-          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
-          else hipLaunchKernelGGL(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
+          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
+          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
+          else ITSD_LAUNCH(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
           return hipGetLastError();
         }
         if (g_gn_reg == 2 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 <= GNS_MAXC &&
             (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
-          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
-          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
-          else hipLaunchKernelGGL(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
+          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
+          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
+          else ITSD_LAUNCH(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
           return hipGetLastError();
         }
         if (g_gn_reg && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
             (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
           if ((g_conv_dbg & 4096) && a.Wout == 32) {  // measurement builds of the W = 32 kernel only
             switch ((g_conv_dbg >> 13) & 127) {
-              case 1: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 1>), gw, dim3(512), 0, s, a); break;
-              case 2: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 2>), gw, dim3(512), 0, s, a); break;
-              case 4: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 4>), gw, dim3(512), 0, s, a); break;
-              case 8: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 8>), gw, dim3(512), 0, s, a); break;
-              case 16: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 16>), gw, dim3(512), 0, s, a); break;
-              case 6: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 6>), gw, dim3(512), 0, s, a); break;
-              case 14: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 14>), gw, dim3(512), 0, s, a); break;
-              case 30: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 30>), gw, dim3(512), 0, s, a); break;
-              case 24: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 24>), gw, dim3(512), 0, s, a); break;
-              case 32: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 32>), gw, dim3(512), 0, s, a); break;
-              case 64: hipLaunchKernelGGL((conv3x3_gn_reg_kernel<32, 64>), gw, dim3(512), 0, s, a); break;
+              case 1: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 1>), gw, dim3(512), 0, s, a); break;
+              case 2: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 2>), gw, dim3(512), 0, s, a); break;
+              case 4: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 4>), gw, dim3(512), 0, s, a); break;
+              case 8: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 8>), gw, dim3(512), 0, s, a); break;
+              case 16: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 16>), gw, dim3(512), 0, s, a); break;
+              case 6: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 6>), gw, dim3(512), 0, s, a); break;
+              case 14: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 14>), gw, dim3(512), 0, s, a); break;
+              case 30: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 30>), gw, dim3(512), 0, s, a); break;
+              case 24: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 24>), gw, dim3(512), 0, s, a); break;
+              case 32: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 32>), gw, dim3(512), 0, s, a); break;
+              case 64: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 64>), gw, dim3(512), 0, s, a); break;
               default: return hipErrorInvalidValue;
             }
             return hipGetLastError();
           }
-          if (a.Wout == 32) hipLaunchKernelGGL(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
-          else if (a.Wout == 16) hipLaunchKernelGGL(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
-          else hipLaunchKernelGGL(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
+          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
+          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
+          else ITSD_LAUNCH(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
           return hipGetLastError();
         }
-        if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
+        if (segs == 1) ITSD_LAUNCH(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
+        else ITSD_LAUNCH(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
         return hipGetLastError();
       }
       dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
       const int THs = std::min(a.Hout, 128 / a.Wout), segs = 128 / (THs * a.Wout);
-      if (segs == 1) hipLaunchKernelGGL(conv3x3_gn_kernel<1>, grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL(conv3x3_gn_kernel<2>, grid, dim3(256), 0, s, a);
+      if (segs == 1) ITSD_LAUNCH(conv3x3_gn_kernel<1>, grid, dim3(256), 0, s, a);
+      else ITSD_LAUNCH(conv3x3_gn_kernel<2>, grid, dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }
@@ -2923,7 +2923,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
     if (g_small_conv && conv_small_ok(a) && (g_small_conv == 2 || (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024))) {
-      hipLaunchKernelGGL(conv_small, dim3((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B), dim3(256), 0, s, a);
+      ITSD_LAUNCH(conv_small, dim3((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B), dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }
@@ -2934,7 +2934,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.subpix) {
     if (!pipe || !lin || a.ksize != 2 || (a.Hout * a.Wout) % 128) return hipErrorInvalidValue;
     grid.z = 4;
-    hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+    ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
   if (pipe && v != 1 && a.splitk_ws && g_splitk) {
@@ -2948,17 +2948,17 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
     grid.z = S < 1 ? 1 : S;
   }
-  if (!pipe || v == 1) hipLaunchKernelGGL(conv_igemm<T>, grid, dim3(256), 0, s, a);
-  else if (v == 2 && lin) hipLaunchKernelGGL((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
-  else if (v == 2) hipLaunchKernelGGL((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
-  else if (v == 3 && lin) hipLaunchKernelGGL((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
-  else if (v == 3) hipLaunchKernelGGL((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
-  else if (lin) hipLaunchKernelGGL((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
+  if (!pipe || v == 1) ITSD_LAUNCH(conv_igemm<T>, grid, dim3(256), 0, s, a);
+  else if (v == 2 && lin) ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+  else if (v == 2) ITSD_LAUNCH((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
+  else if (v == 3 && lin) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
+  else if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
+  else if (lin) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
+  else ITSD_LAUNCH((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
   if (grid.z > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(splitk_epilogue_kernel<T>, dim3(grid.x, grid.y), dim3(256), 0, s, a, (int)grid.z);
+    ITSD_LAUNCH(splitk_epilogue_kernel<T>, dim3(grid.x, grid.y), dim3(256), 0, s, a, (int)grid.z);
   }
   return hipGetLastError();
 }

@@ -102,7 +102,7 @@ hipError_t launch_groupnorm(const GNArgs& a0, int n, hipStream_t s) {
   const long long total = (long long)a.HW * ((a.C1 + a.C2) / EPC);
   a.chunks_per_block = 1024;
   const int bpi = (int)((total + a.chunks_per_block - 1) / a.chunks_per_block);
-  hipLaunchKernelGGL(gn_apply_kernel<T>, dim3(bpi, n), dim3(256), 0, s, a);
+  ITSD_LAUNCH(gn_apply_kernel<T>, dim3(bpi, n), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 template hipError_t launch_groupnorm<float>(const GNArgs&, int, hipStream_t);
@@ -368,9 +368,9 @@ hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
     if (a.vt && a.S > 256) {
       if (!attn_flash_ok(a.S, a.C)) return hipErrorInvalidValue;
       const dim3 grid((a.S + 127) / 128, n);
-      if (a.C == 64) hipLaunchKernelGGL(attn_flash_kernel<2>, grid, dim3(256), 0, s, a);
-      else if (a.C == 128) hipLaunchKernelGGL(attn_flash_kernel<4>, grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL(attn_flash_kernel<8>, grid, dim3(256), 0, s, a);
+      if (a.C == 64) ITSD_LAUNCH(attn_flash_kernel<2>, grid, dim3(256), 0, s, a);
+      else if (a.C == 128) ITSD_LAUNCH(attn_flash_kernel<4>, grid, dim3(256), 0, s, a);
+      else ITSD_LAUNCH(attn_flash_kernel<8>, grid, dim3(256), 0, s, a);
       return hipGetLastError();
     }
     if (a.vt) {
@@ -382,13 +382,13 @@ hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr = true;
       }
-      hipLaunchKernelGGL(attn_mfma_kernel, dim3((a.S + ATT_AQ - 1) / ATT_AQ, n), dim3(256), sm, s, a);
+      ITSD_LAUNCH(attn_mfma_kernel, dim3((a.S + ATT_AQ - 1) / ATT_AQ, n), dim3(256), sm, s, a);
       return hipGetLastError();
     }
   }
   const int qc = att_qc(a.S);
   dim3 grid((a.S + qc - 1) / qc, n);
-  hipLaunchKernelGGL(attn_kernel<T>, grid, dim3(256), qc * a.S * sizeof(float), s, a);
+  ITSD_LAUNCH(attn_kernel<T>, grid, dim3(256), qc * a.S * sizeof(float), s, a);
   return hipGetLastError();
 }
 template hipError_t launch_attn<float>(const AttnArgs&, int, hipStream_t);
@@ -498,7 +498,7 @@ hipError_t launch_head(const HeadArgs& a, hipStream_t s) {
   if (a.Cout % EPC || cq > 256 || 256 % cq || HW % G || (G % a.W && a.W % G)) return hipErrorInvalidValue;
   const int TW = (a.W <= G ? a.W : G) + 2, TR = (a.W <= G ? G / a.W : 1) + 2;
   const size_t smem = ((size_t)a.Cout * 28 + (size_t)(256 / cq) * a.Cout * 2 + 3 * TR * TW) * sizeof(float);
-  hipLaunchKernelGGL(head_kernel<T>, dim3((unsigned)((long long)a.n * HW / G)), dim3(256), smem, s, a);
+  ITSD_LAUNCH(head_kernel<T>, dim3((unsigned)((long long)a.n * HW / G)), dim3(256), smem, s, a);
   return hipGetLastError();
 }
 template hipError_t launch_head<float>(const HeadArgs&, hipStream_t);
@@ -861,7 +861,7 @@ hipError_t launch_tail_mfma(const TailArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(tail_mfma_kernel, dim3(a.n * (a.H / (TM_PX / a.W))), dim3(256), tail_mfma_smem(a.H, a.W, a.C), s,
+  ITSD_LAUNCH(tail_mfma_kernel, dim3(a.n * (a.H / (TM_PX / a.W))), dim3(256), tail_mfma_smem(a.H, a.W, a.C), s,
                      a);
   return hipGetLastError();
 }
@@ -878,11 +878,11 @@ hipError_t launch_tail(const TailArgs& a, hipStream_t s) {
       if (e != hipSuccess) return e;
       attr = true;
     }
-    hipLaunchKernelGGL(tail2_kernel<T>, dim3(a.n * (a.H / (64 / a.W))), dim3(256), sm, s, a);
+    ITSD_LAUNCH(tail2_kernel<T>, dim3(a.n * (a.H / (64 / a.W))), dim3(256), sm, s, a);
     return hipGetLastError();
   }
   const long long total = (long long)a.n * a.H * a.W;
-  hipLaunchKernelGGL(tail_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 27 * a.C * sizeof(float), s, a);
+  ITSD_LAUNCH(tail_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 27 * a.C * sizeof(float), s, a);
   return hipGetLastError();
 }
 template hipError_t launch_tail<float>(const TailArgs&, hipStream_t);
@@ -926,12 +926,12 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* in, int M, int
 
 hipError_t launch_emb_input(const int* idx, int M, const float* freq, const float* table, int d, float* out,
                             int idx_offset, hipStream_t s) {
-  hipLaunchKernelGGL(emb_input_kernel, dim3(M), dim3(128), 0, s, idx, M, freq, table, d, out, idx_offset);
+  ITSD_LAUNCH(emb_input_kernel, dim3(M), dim3(128), 0, s, idx, M, freq, table, d, out, idx_offset);
   return hipGetLastError();
 }
 hipError_t launch_linear(const float* in, int M, int Nin, const float* Wt, const float* b, int Nout, int silu_in,
                          float* out, hipStream_t s) {
-  hipLaunchKernelGGL(linear_kernel, dim3((Nout + 255) / 256, M), dim3(256), Nin * sizeof(float), s, in, M, Nin, Wt,
+  ITSD_LAUNCH(linear_kernel, dim3((Nout + 255) / 256, M), dim3(256), Nin * sizeof(float), s, in, M, Nin, Wt,
                      b, Nout, silu_in, out);
   return hipGetLastError();
 }
@@ -1035,7 +1035,7 @@ __global__ __launch_bounds__(256) void verify_kernel(int kind, const float* imag
 
 hipError_t launch_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w, double* scores,
                          hipStream_t s) {
-  hipLaunchKernelGGL(verify_kernel, dim3(n_cand), dim3(256), 0, s, kind, images, b, c, h, w, scores);
+  ITSD_LAUNCH(verify_kernel, dim3(n_cand), dim3(256), 0, s, kind, images, b, c, h, w, scores);
   return hipGetLastError();
 }
 
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(256) void noise_kernel(float* out, const float* piv
 hipError_t launch_noise(float* out, const float* pivot, int n_cand, long long per_cand, float scale,
                         unsigned long long seed, unsigned stream_id, long long cand_offset, hipStream_t s) {
   const long long total = (long long)n_cand * per_cand;
-  hipLaunchKernelGGL(noise_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, pivot, total, per_cand,
+  ITSD_LAUNCH(noise_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, pivot, total, per_cand,
                      scale, seed, stream_id, cand_offset * per_cand);
   return hipGetLastError();
 }
@@ -1066,16 +1066,16 @@ __global__ void run_begin_kernel(int* t, int t_begin, int* nan_flag, RunParams* 
   *run = v;
 }
 hipError_t launch_run_begin(int* t, int t_begin, int* nan_flag, RunParams* run, const RunParams& v, hipStream_t s) {
-  hipLaunchKernelGGL(run_begin_kernel, dim3(1), dim3(1), 0, s, t, t_begin, nan_flag, run, v);
+  ITSD_LAUNCH(run_begin_kernel, dim3(1), dim3(1), 0, s, t, t_begin, nan_flag, run, v);
   return hipGetLastError();
 }
 __global__ void add_int_kernel(int* p, int v) { *p += v; }
 hipError_t launch_set_int(int* p, int v, hipStream_t s) {
-  hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
+  ITSD_LAUNCH(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
   return hipGetLastError();
 }
 hipError_t launch_add_int(int* p, int v, hipStream_t s) {
-  hipLaunchKernelGGL(add_int_kernel, dim3(1), dim3(1), 0, s, p, v);
+  ITSD_LAUNCH(add_int_kernel, dim3(1), dim3(1), 0, s, p, v);
   return hipGetLastError();
 }
 

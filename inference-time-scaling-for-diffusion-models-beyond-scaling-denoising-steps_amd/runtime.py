@@ -70,6 +70,7 @@ _SIGS = {
                          ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
     "itsd_set_option": [ctypes.c_char_p, ctypes.c_int],
     "itsd_unet_query": [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)],
+    "itsd_kernel_name": [ctypes.c_int],
     "itsd_last_error": [],
     "itsd_version": [],
 }
@@ -87,7 +88,7 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = ctypes.c_char_p if name == "itsd_last_error" else ctypes.c_int
+            f.restype = ctypes.c_char_p if name in ("itsd_last_error", "itsd_kernel_name") else ctypes.c_int
         _lib = L
     return _lib
 
@@ -209,7 +210,15 @@ class NativeUNet:
                                      ctypes.byref(n), stream_ptr(x.device)))
         k = n.value
         names = {0: "gn", 1: "conv", 2: "attn", 3: "gncoef", 4: "convgn", 5: "convgnw", 6: "convgnw4", -1: "head", -2: "tail"}
-        return [{"kind": names.get(int(kinds[i]), str(kinds[i])), "ms": float(ms[i]), "flops": float(fl[i]),
+        L = lib()
+
+        def decode(v: int):  # (kernel id << 8) | op class as a signed byte
+            base = v & 0xFF
+            base = base - 256 if base >= 128 else base
+            return names.get(base, str(base)), L.itsd_kernel_name(v >> 8).decode()
+
+        dec = [decode(int(kinds[i])) for i in range(k)]
+        return [{"kind": dec[i][0], "kernel": dec[i][1], "ms": float(ms[i]), "flops": float(fl[i]),
                  "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
                  "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5])} for i in range(k)]
 

@@ -74,7 +74,7 @@ def main():
     for i, o in enumerate(ops):
         tf = o["flops"] / (o["ms"] * 1e-3) / 1e12 if o["ms"] > 0 and o["flops"] > 0 else 0.0
         print(f"{i:3d} {o['kind']:5} {o['M']:7d} {o['N']:5d} {o['K']:5d} {o['H']:3d} {o['ks']:2d} {o['stride_up']:3d} "
-              f"{o['ms']:8.4f} {tf:7.1f}")
+              f"{o['ms']:8.4f} {tf:7.1f}  {o.get('kernel', '')}")
         key = o["kind"] if o["kind"] not in CONV_KINDS else f"{o['kind']} H{o['H']}"
         agg[key][0] += 1
         agg[key][1] += o["ms"]

@@ -5,6 +5,7 @@ MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KiB in rocprofv3's derived coun
 Infinity-Cache hits are included in these memory-side counts.
 
     python tools/pmc_traffic.py gpurun_out/pmc convgn [out.json]
+    python tools/pmc_traffic.py gpurun_out/pmc "conv3x3_gn_pws_kernel<32>" [out.json]
 """
 import csv
 import glob
@@ -13,10 +14,10 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILIES = {
+FAMILIES = {  # census op classes; any other argument is taken as a kernel-name substring
     "convgn": ("conv3x3_gn_kernel",),
-    "convgnw": ("conv3x3_gn_wide_kernel<1>", "conv3x3_gn_wide_kernelILi1E"),
-    "convgnw4": ("conv3x3_gn_wide_kernel<4>", "conv3x3_gn_wide_kernelILi4E"),
+    "convgnw": ("conv3x3_gn_pws_kernel<32>", "conv3x3_gn_pws_kernel<16>"),
+    "convgnw4": ("conv3x3_gn_pws_kernel<8>",),
     "conv": ("conv_pipe", "conv_small", "splitk_epilogue_kernel", "splitk_wide_epilogue_kernel"),
 }
 
@@ -24,7 +25,7 @@ FAMILIES = {
 def main():
     d, fam = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else None
-    pats = FAMILIES[fam]
+    pats = FAMILIES.get(fam, (fam,))
     per = defaultdict(dict)
     names = {}
     for f in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
