@@ -183,10 +183,16 @@ def windowed_rate(smp, n: int, img: int, T: int, window: int, labels=None, round
     return n / (T * ms_step * 1e-3), ms_step
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (long runs must show life within minutes; stdout is the JSON)."""
+    print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def leg(name, make_net, n: int, img: int, T: int, window: int, cfg: bool, precision: str = "bf16",
         workload: str = ""):
     from itsd.diffusion import CondGaussianDiffusionSampler, GaussianDiffusionSampler
 
+    progress(f"leg {name}: {workload}")
     net = make_net()
     net.reserve(2 * n if cfg else n)
     if cfg:
@@ -256,6 +262,8 @@ def main():
     eng = SearchEngine(smp, OracleVerifier(), seed=1234, graph=not args.no_graph)
     shape = (1, 3, 32, 32)
 
+    if rank == 0:
+        progress(f"warmup x{args.warmup}, then {args.steps} timed rounds of N={n_total}")
     for w in range(args.warmup):
         eng.run_round(10_000 + w, n_total, shape)
     torch.cuda.synchronize()
@@ -277,6 +285,7 @@ def main():
 
     roof = None
     if rank == 0:
+        progress(f"headline: {n_total * args.steps / dt:.3f} candidate-images/s; roofline census")
         ops, agg, nat, x, t = census(net, n_local, 32)
         kernel, roof = dominant_roofline(ops, agg, nat, x, t, args.precision)
         n_l = roof["launches_per_forward"]
@@ -324,6 +333,7 @@ def main():
         for n, window in ((64, 1000), (1024, 100)):
             if n == n_local:
                 continue
+            progress(f"sweep N={n}")
             net.reserve(n)
             rate, ms = windowed_rate(smp, n, 32, args.T, window)
             sweep[str(n)] = {"value": round(rate, 3), "ms_per_step": round(ms, 3),
@@ -359,6 +369,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         cpu = cpu_baseline(args.T, seconds=args.cpu_seconds)
 
     if rank == 0:
