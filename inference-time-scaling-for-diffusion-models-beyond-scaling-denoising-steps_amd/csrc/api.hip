@@ -951,7 +951,7 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_reg")) {
-    if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "gn_reg in [0,3]");
+    if (value < 0 || value > 4) return fail(ITSD_ERR_INVALID, "gn_reg in [0,4]");
     itsd::g_gn_reg = value;
     return ITSD_OK;
   }

@@ -39,6 +39,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// two floats -> one word of two bf16 (lo in the low half): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  const b2v r = __builtin_convertvector((f2v){lo, hi}, b2v);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static __device__ __forceinline__ float load(const float* p) { return *p; }

@@ -55,7 +55,8 @@ int main() {
   expect("set_option splitk=-1", itsd_set_option("splitk", -1), ITSD_ERR_INVALID);
   expect("set_option small_conv=3", itsd_set_option("small_conv", 3), ITSD_ERR_INVALID);
   expect("set_option gn_wide=7", itsd_set_option("gn_wide", 7), ITSD_ERR_INVALID);
-  expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_ERR_INVALID);
+  expect("set_option gn_reg=5", itsd_set_option("gn_reg", 5), ITSD_ERR_INVALID);
+  expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option gn_reg=3", itsd_set_option("gn_reg", 3), ITSD_OK);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it

@@ -324,7 +324,7 @@ def test_wide_tile_convs_bit_identical_and_vs_oracle(n):
     with torch.no_grad():
         ref = _oracle(a, synthetic_state_dict(a, 0))(x, t)
     regs = {}
-    for v in (1, 2, 3):  # conv3x3_gn_reg_kernel, _ws_kernel (halo waves), _pws_kernel (persistent)
+    for v in (1, 2, 3, 4):  # conv3x3_gn_reg_kernel, _ws_kernel (halo waves), _pws_kernel (persistent), _p4_kernel
         reg = _eps_with(net, xd, td, gn_wide=2, conv_wide=2, splitk=0, gn_reg=v)
         assert torch.equal(reg, _eps_with(net, xd, td, gn_wide=2, conv_wide=2, splitk=0, gn_reg=v))
         print(f"gn_reg={v}: rel-L2 vs oracle: narrow {_rel_l2(narrow, ref):.3e} reg {_rel_l2(reg, ref):.3e}; "

@@ -6,6 +6,8 @@ hipcc -DITSD_STAMPS, see conv.hip; per wave, s_memtime cycles). Never part of th
 ITSD_GN_REG selects the kernel (itsd_set_option "gn_reg"):
   0 -> conv3x3_gn_wide_kernel: wait / barrier / weight-DMA issue / MFMA issue / GN transform,
        prologue, epilogue, total (8 waves);
+  3 -> conv3x3_gn_pws_kernel (persistent): MFMA waves 0..7, halo waves 8..11;
+  4 -> conv3x3_gn_p4_kernel (persistent, one MFMA wave per SIMD): MFMA waves 0..3, halo 4..7;
   2 -> conv3x3_gn_ws_kernel: MFMA waves 0..7 (chunk compute, barrier wait, prologue, epilogue,
        total) and halo waves 8..11 (halo staging, barrier wait, chunk-0 staging, output pass, total).
 """
@@ -45,20 +47,21 @@ for i in sel:
     nb = min(1024, (o["M"] // 256) * (o["N"] // 128))
     st = st[:nb]
     chunks = o["K"] // (9 * 64)
-    if GN_REG == 3:
+    if GN_REG in (3, 4):
+        NM = 8 if GN_REG == 3 else 4  # MFMA waves; the 4 halo waves follow
         tiles = (o["M"] // 256) * (o["N"] // 128)
         G = min(tiles, 256)
         st = buf.reshape(1024, 16, 8).astype(np.float64)[:G]
-        tot = st[:, :8, 7].mean()
+        tot = st[:, :NM, 7].mean()
         tpb = tiles / G
         print(f"op {i:3d} {o['kind']:8s} M={o['M']} N={o['N']} K={o['K']} H={o['H']}: {ms*1e3:.1f} us/launch, "
               f"block {tot:.0f} memtime ticks, {tpb:.2f} tiles x {chunks} chunks per block")
-        m = st[:, :8]
+        m = st[:, :NM]
         print("   MFMA waves: " + "  ".join(f"{n}={m[:, :, k].mean():.0f} ({100*m[:, :, k].mean()/tot:.0f}%)"
                                            for k, n in ((0, "compute"), (1, "barrier"), (6, "epilogue"))))
         print(f"     per chunk: compute={m[:, :, 0].mean()/(chunks*tpb):.0f}  barrier={m[:, :, 1].mean()/(chunks*tpb):.0f}"
               f"  epilogue/tile={m[:, :, 6].mean()/tpb:.0f}")
-        h = st[:, 8:12]
+        h = st[:, NM:NM + 4]
         print("   halo waves: " + "  ".join(f"{n}={h[:, :, k].mean():.0f} ({100*h[:, :, k].mean()/tot:.0f}%)"
                                            for k, n in ((3, "transform"), (1, "barrier"), (5, "prologue"))))
         print(f"     per stage: transform={h[:, :, 3].mean()/(chunks*tpb):.0f}")
