@@ -955,6 +955,15 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_gn_reg = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "small_korder")) {  // conv_small K order: 1 taps inside each channel chunk, 0 tap-major
+    itsd::g_small_korder = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p4_w")) {  // levels gn_reg = 4 applies to (bit 0 W = 8, 1 W = 16, 2 W = 32); others pws
+    if (value < 0 || value > 7) return fail(ITSD_ERR_INVALID, "p4_w in [0,7]");
+    itsd::g_p4_w = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
     itsd::g_fuse_gn = value ? 1 : 0;
     return ITSD_OK;

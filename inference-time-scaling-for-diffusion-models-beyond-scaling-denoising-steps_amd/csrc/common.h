@@ -12,6 +12,8 @@ extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
 extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
 extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option "gn_reg")
+extern int g_small_korder;  // conv_small K order (itsd_set_option "small_korder")
+extern int g_p4_w;          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
 extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)

@@ -43,10 +43,12 @@ int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
-int g_gn_reg = 3;        // fused GroupNorm conv with the weights streamed into registers where the
+int g_gn_reg = 4;        // fused GroupNorm conv with the weights streamed into registers where the
                          // 256-pixel tile applies: 0 off, 1 conv3x3_gn_reg_kernel, 2 warp-specialized
                          // conv3x3_gn_ws_kernel (halo waves), 3 persistent conv3x3_gn_pws_kernel,
                          // 4 persistent with one MFMA wave per SIMD (conv3x3_gn_p4_kernel)
+int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel chunk, 0 tap-major (default: 1 measured 2-3 % slower)
+int g_p4_w = 7;         // levels conv3x3_gn_p4_kernel takes under gn_reg = 4: bit 0 W = 8, 1 W = 16, 2 W = 32
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
                          // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
@@ -524,6 +526,11 @@ constexpr int SM_NS = 4;
 constexpr int SM_EPI = SM_B * (SM_B + 4) * 4 + SM_B * SM_B * 4;  // E + (addv | statistics groups)
 constexpr int SM_SMEM = (SM_NS * 2 * SM_TILEB > SM_EPI) ? SM_NS * 2 * SM_TILEB : SM_EPI;
 
+// TAPIN: the K loop runs the taps inside each 64-channel chunk (K-chunk kc = chunk * taps + tap)
+// instead of the weight layout's tap-major order: a chunk's input rows are re-read by the 9 taps
+// in 9 consecutive stages (L2 / L1 hits) instead of once per tap sweep over the whole Cin (a reuse
+// distance of Cin/64 stages x every resident block's rows: ~4 MiB per XCD at the 4x4 level, N = 256)
+template <bool TAPIN>
 __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
   typedef bf16_t T;
   constexpr int BK = 64, STAGE = 2 * SM_TILEB;
@@ -560,8 +567,17 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       }
     tmask[q] = m;
   }
+  const int ntap = a.ksize * a.ksize;
   auto issue = [&](int kc) {
-    const int tap = kc / cpt, ci0 = (kc - tap * cpt) * BK;
+    int tap, ci0;
+    if constexpr (TAPIN) {
+      const int cc = kc / ntap;
+      tap = kc - cc * ntap;
+      ci0 = cc * BK;
+    } else {
+      tap = kc / cpt;
+      ci0 = (kc - tap * cpt) * BK;
+    }
     const int ky = tap / a.ksize, kx = tap - ky * a.ksize;
     char* sA = smem + (kc % SM_NS) * STAGE;
     char* sB = sA + SM_TILEB;
@@ -570,7 +586,7 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
     const int toff = (ky * a.Win + kx) * (s1 ? a.C1 : a.C2) + (s1 ? ci0 : ci0 - a.C1);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const T* ga = arow[q] ? arow[q] + (size_t)kc * BK : zero;
+      const T* ga = arow[q] ? arow[q] + (size_t)(tap * Cin + ci0) : zero;
       __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sA + (2 * wid + q) * 1024), 16, 0, 0);
     }
 #pragma unroll
@@ -2664,7 +2680,10 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
     }
     // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
     // issued after it, may still be in flight)
-    if (res) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
+    if (res) {  // (last stage: nothing was issued after the DMA)
+      if (q + 1 < nstages) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #ifdef ITSD_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -2687,7 +2706,8 @@ __global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
 // budget. Here a 512-thread block runs 4 MFMA waves (one per SIMD, 64 couts x 128 pixels each:
 // 8 MFMAs per k-step, half the B reads per MFMA, 128 accumulators in AGPRs) beside the same 4
 // halo waves: 2 waves per SIMD, 256 registers each.
-constexpr int P4_RING = 5;  // A k-step slots (prefetch distance 4 k-steps = 32 MFMAs)
+constexpr int P4_RING = 6;  // A k-step slots (prefetch distance 5 k-steps = 40 MFMAs); divides the 36 k-steps
+                            // of a chunk, so the slots of the next chunk's prefetched steps line up
 constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 MFMAs ahead)
 template <int W, int AB = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
@@ -2700,7 +2720,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  constexpr int RING = (AB & 64) ? P4_RING + 1 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
+  constexpr int RING = (AB & 64) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
+  static_assert(36 % RING == 0, "ring slots repeat per chunk");
   __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4];
   char* const rlds = smem + 2 * HALO;
   float* const addv = (float*)(smem + 2 * HALO + RESB);  // [2 tile parities][NSEG][128]
@@ -3255,7 +3276,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     }
     // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
     // issued after it, may still be in flight)
-    if (res) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
+    if (res) {  // (last stage: nothing was issued after the DMA)
+      if (q + 1 < nstages) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #ifdef ITSD_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -3480,7 +3504,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
         const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
         if (g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
-            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
+            ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)))) {
           // persistent, one MFMA wave per SIMD (512 threads, 256 registers a wave)
           const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
           const dim3 gp(std::min(tiles, g_num_cus));
@@ -3504,7 +3528,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }
-        if (g_gn_reg == 3 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
+        if (g_gn_reg >= 3 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
             (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
           // persistent: one block per CU (160 KiB of LDS each), tiles strided over the grid
           const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
@@ -3580,7 +3604,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
     if (g_small_conv && conv_small_ok(a) && (g_small_conv == 2 || (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024))) {
-      ITSD_LAUNCH(conv_small, dim3((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B), dim3(256), 0, s, a);
+      const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
+      if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);
+      else ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }

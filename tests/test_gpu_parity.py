@@ -285,7 +285,7 @@ def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt):
         assert (out - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
 
 
-_TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 3}
+_TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 4}
 
 
 def _eps_with(net, x, t, **opts):
