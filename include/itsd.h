@@ -17,6 +17,8 @@
  *   itsd_verify                  <- OracleVerifier / SelfSupervisedVerifier /
  *                                   AestheticPredictor .score (search/verifier.py:45-66,
  *                                   223-248, 262-287), batched per candidate
+ *   itsd_verify_paired           <- SelfSupervisedVerifier.score(images, reference_features)
+ *                                   (search/verifier.py:235-240)
  *   itsd_attention               <- AttnBlock core softmax(q k^T C^-0.5) v
  *                                   (Diffusion/Model.py:152-161, ModelCondition.py:105-115)
  *   itsd_profile_forward / _ops / _op, itsd_unet_query, itsd_set_option
@@ -54,7 +56,7 @@ extern "C" {
 
 enum { ITSD_ARCH_DDPM = 0, ITSD_ARCH_CFG = 1 };
 enum { ITSD_PREC_FP32 = 0, ITSD_PREC_BF16 = 1 };
-enum { ITSD_VERIFY_ORACLE = 0, ITSD_VERIFY_SELFSUP = 1, ITSD_VERIFY_AESTHETIC = 2 };
+enum { ITSD_VERIFY_ORACLE = 0, ITSD_VERIFY_SELFSUP = 1, ITSD_VERIFY_AESTHETIC = 2, ITSD_VERIFY_MEAN = 3 };
 
 /* itsd_sampler_run flags */
 #define ITSD_RUN_GRAPH 1u   /* capture one denoising step in a hipGraph and replay it */
@@ -115,9 +117,17 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
 int itsd_noise(float* out, const float* pivot, int n_cand, int64_t per_cand, float scale, uint64_t seed,
                uint32_t stream_id, int64_t cand_offset, void* stream);
 
-/* scores[c] = verifier(images[c*b:(c+1)*b]) for c < n_cand; images NCHW fp32. */
+/* scores[c] = verifier(images[c*b:(c+1)*b]) for c < n_cand; images NCHW fp32.
+ * ITSD_VERIFY_MEAN is OracleVerifier.score with dataset_stats (search/verifier.py:66: mean). */
 int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w,
                 double* scores, void* stream);
+
+/* SelfSupervisedVerifier.score(images, reference_features) (search/verifier.py:235-240):
+ * scores[i] = cos(pool8x8(images[i]), ref_features[i]) for i < n_cand (one image per
+ * candidate: the reference's .item() of the per-image vector needs a single image);
+ * ref_features [n_cand][c*64] fp32. */
+int itsd_verify_paired(const float* images, const float* ref_features, int n_cand, int c, int h, int w,
+                       double* scores, void* stream);
 
 /* AttnBlock core on n images of S tokens, width C (single head):
  *   out[i][s][:] = softmax_j(q_s . k_j * C^-0.5) v_j

@@ -31,7 +31,7 @@ template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
 hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
 hipError_t launch_linear(const float*, int, int, const float*, const float*, int, int, float*, hipStream_t);
-hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, hipStream_t);
+hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, const float*, hipStream_t);
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
 hipError_t launch_run_begin(int*, int, int*, RunParams*, const RunParams&, hipStream_t);
@@ -1168,10 +1168,18 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
 
 int itsd_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w, double* scores, void* stream) {
   if (!images || !scores || n_cand < 1 || b < 1) return fail(ITSD_ERR_INVALID, "bad verify arguments");
-  if (kind < 0 || kind > 2) return fail(ITSD_ERR_INVALID, "unknown verifier kind");
+  if (kind < 0 || kind > 3) return fail(ITSD_ERR_INVALID, "unknown verifier kind");
   if (kind == ITSD_VERIFY_SELFSUP && (c * 64 > 192 || h % 8 || w % 8 || b > 64))
     return fail(ITSD_ERR_INVALID, "selfsup verifier needs c<=3, h,w divisible by 8, b<=64");
-  HIPCHK(launch_verify(kind, images, n_cand, b, c, h, w, scores, (hipStream_t)stream));
+  HIPCHK(launch_verify(kind, images, n_cand, b, c, h, w, scores, nullptr, (hipStream_t)stream));
+  return ITSD_OK;
+}
+
+int itsd_verify_paired(const float* images, const float* ref_features, int n_cand, int c, int h, int w,
+                       double* scores, void* stream) {
+  if (!images || !ref_features || !scores || n_cand < 1) return fail(ITSD_ERR_INVALID, "bad verify arguments");
+  if (c * 64 > 192 || h % 8 || w % 8) return fail(ITSD_ERR_INVALID, "paired selfsup needs c<=3, h,w divisible by 8");
+  HIPCHK(launch_verify(4, images, n_cand, 1, c, h, w, scores, ref_features, (hipStream_t)stream));
   return ITSD_OK;
 }
 

@@ -943,7 +943,7 @@ hipError_t launch_linear(const float* in, int M, int Nin, const float* Wt, const
 //  AESTHETIC verifier.py:277-286 if min<0: x=(x+1)/2 ; 2 * mean_b std_unbiased(x_b)
 //  SELFSUP   verifier.py:219-246 avgpool 8x8 -> L2 normalise -> mean off-diagonal cosine
 __global__ __launch_bounds__(256) void verify_kernel(int kind, const float* images, int b, int c, int h, int w,
-                                                     double* scores) {
+                                                     double* scores, const float* ref) {
   const int cand = blockIdx.x;
   const int D = c * h * w;
   const float* base = images + (size_t)cand * b * D;
@@ -958,6 +958,13 @@ __global__ __launch_bounds__(256) void verify_kernel(int kind, const float* imag
     __syncthreads();
     return red[0] + red[1] + red[2] + red[3];
   };
+  if (kind == 3) {  // OracleVerifier with dataset stats (verifier.py:66): mean of the candidate's images
+    double s = 0.0;
+    for (long long i = tid; i < (long long)b * D; i += 256) s += base[i];
+    s = block_sum(s);
+    if (tid == 0) scores[cand] = (double)(float)(s / ((double)b * D));
+    return;
+  }
   if (kind == 0 || kind == 2) {
     bool shift = false;
     if (kind == 2) {
@@ -1017,6 +1024,19 @@ __global__ __launch_bounds__(256) void verify_kernel(int kind, const float* imag
     for (int f = 0; f < F; ++f) feat[tid][f] = feat[tid][f] / nrm;
   }
   __syncthreads();
+  if (kind == 4) {  // paired mode (verifier.py:237-240): cosine of image i with reference row i
+    // one candidate = one image (the reference's .item() of a b-vector needs b == 1)
+    const float* r = ref + (size_t)cand * F;
+    double rr = 0.0, fr = 0.0;
+    for (int f = tid; f < F; f += 256) {
+      rr += (double)r[f] * r[f];
+      fr += (double)feat[0][f] * r[f];
+    }
+    rr = block_sum(rr);
+    fr = block_sum(fr);
+    if (tid == 0) scores[cand] = (double)(float)(fr / fmax(sqrt(rr), 1e-12));
+    return;
+  }
   double s = 0.0;
   for (int pr = tid; pr < b * b; pr += 256) {
     const int i = pr / b, j = pr % b;
@@ -1034,8 +1054,8 @@ __global__ __launch_bounds__(256) void verify_kernel(int kind, const float* imag
 }
 
 hipError_t launch_verify(int kind, const float* images, int n_cand, int b, int c, int h, int w, double* scores,
-                         hipStream_t s) {
-  ITSD_LAUNCH(verify_kernel, dim3(n_cand), dim3(256), 0, s, kind, images, b, c, h, w, scores);
+                         const float* ref, hipStream_t s) {
+  ITSD_LAUNCH(verify_kernel, dim3(n_cand), dim3(256), 0, s, kind, images, b, c, h, w, scores, ref);
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("ITSD_LIB") or os.path.join(_HERE, "libitsd_hip.so")
 
 ITSD_OK, ITSD_ERR_INVALID, ITSD_ERR_HIP, ITSD_ERR_WEIGHTS, ITSD_ERR_NAN, ITSD_ERR_OOM = range(6)
 PREC_FP32, PREC_BF16 = 0, 1
-VERIFY_ORACLE, VERIFY_SELFSUP, VERIFY_AESTHETIC = 0, 1, 2
+VERIFY_ORACLE, VERIFY_SELFSUP, VERIFY_AESTHETIC, VERIFY_MEAN = 0, 1, 2, 3
 RUN_GRAPH, RUN_CLIP, RUN_SYNC = 1, 2, 4
 
 
@@ -58,6 +58,8 @@ _SIGS = {
                    ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p],
     "itsd_verify": [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                     ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p],
+    "itsd_verify_paired": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_void_p, ctypes.c_void_p],
     "itsd_attention": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        ctypes.c_int, ctypes.c_void_p],
     "itsd_profile_forward": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -244,6 +246,18 @@ def verify(kind: int, images: torch.Tensor, n_cand: int) -> torch.Tensor:
     scores = torch.empty(n_cand, dtype=torch.float64, device=images.device)
     check(lib().itsd_verify(int(kind), images.data_ptr(), int(n_cand), N // n_cand, C, H, W, scores.data_ptr(),
                             stream_ptr(images.device)))
+    return scores
+
+
+def verify_paired(images: torch.Tensor, ref_features: torch.Tensor) -> torch.Tensor:
+    """Per-image cosine of the 8x8-pooled features with reference feature rows (float64)."""
+    assert images.dtype == torch.float32 and images.is_contiguous() and images.is_cuda
+    N, C, H, W = images.shape
+    ref = ref_features.to(images.device, torch.float32).contiguous()
+    assert ref.shape == (N, C * 64), f"reference features must be [{N}, {C * 64}]"
+    scores = torch.empty(N, dtype=torch.float64, device=images.device)
+    check(lib().itsd_verify_paired(images.data_ptr(), ref.data_ptr(), int(N), C, H, W, scores.data_ptr(),
+                                   stream_ptr(images.device)))
     return scores
 
 

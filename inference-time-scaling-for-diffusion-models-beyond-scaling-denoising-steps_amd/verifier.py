@@ -41,10 +41,13 @@ class OracleVerifier(_NativeVerifier):
     def __init__(self, dataset_stats: Optional[Dict[str, np.ndarray]] = None):
         self.dataset_stats = dataset_stats
 
+    def score_batch(self, images: torch.Tensor, n_cand: int) -> torch.Tensor:
+        # with dataset stats the reference's TODO branch scores the plain mean (verifier.py:66)
+        kind = rt.VERIFY_ORACLE if self.dataset_stats is None else rt.VERIFY_MEAN
+        return rt.verify(kind, _dev(images), n_cand)
+
     def score(self, images: torch.Tensor, labels: Optional[torch.Tensor] = None) -> float:
-        if self.dataset_stats is None:
-            return float(self.score_batch(images, 1)[0].item())
-        return torch.mean(images).item()  # verifier.py:66 (TODO branch of the reference)
+        return float(self.score_batch(images, 1)[0].item())
 
 
 class SelfSupervisedVerifier(_NativeVerifier):
@@ -60,10 +63,11 @@ class SelfSupervisedVerifier(_NativeVerifier):
         return F.adaptive_avg_pool2d(images, (8, 8)).flatten(1)
 
     def score(self, images: torch.Tensor, reference_features: Optional[torch.Tensor] = None) -> float:
-        if reference_features is not None:  # verifier.py:237-240 (paired mode, not batched)
-            f = F.normalize(self.extract_features(images), dim=-1)
-            r = F.normalize(reference_features.to(f.device), dim=-1)
-            return torch.sum(f * r, dim=-1).item()
+        if reference_features is not None:  # verifier.py:237-240: per-image cosine, then .item()
+            images = _dev(images)
+            if images.shape[0] != 1:  # the reference's .item() of a b-vector raises the same way
+                raise RuntimeError(f"a Tensor with {images.shape[0]} elements cannot be converted to Scalar")
+            return float(rt.verify_paired(images, reference_features.reshape(1, -1))[0].item())
         return float(self.score_batch(images, 1)[0].item())
 
 

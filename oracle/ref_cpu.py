@@ -214,6 +214,18 @@ def aesthetic_score(images: Tensor) -> float:
     return (cd + ct).item()
 
 
+def oracle_stats_score(images: Tensor) -> float:
+    """``verifier.py:65-66``: with dataset_stats the reference returns the plain mean."""
+    return torch.mean(images).item()
+
+
+def selfsup_paired_score(images: Tensor, reference_features: Tensor) -> float:
+    """``verifier.py:232-240`` with reference features: per-image cosine, then .item()."""
+    f = F.normalize(F.adaptive_avg_pool2d(images, (8, 8)).flatten(1), dim=-1)
+    r = F.normalize(reference_features, dim=-1)
+    return torch.sum(f * r, dim=-1).item()
+
+
 VERIFIERS = {"oracle": oracle_score, "selfsup": selfsup_score, "aesthetic": aesthetic_score}
 
 

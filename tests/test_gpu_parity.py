@@ -164,6 +164,23 @@ def test_verifiers_vs_reference():
                 assert abs(got - want) <= 1e-5, (case, name, got, want)
 
 
+def test_verifier_branches_vs_reference():
+    """The two verifier branches off the search path run natively too: OracleVerifier with
+    dataset stats (ITSD_VERIFY_MEAN, verifier.py:66) and the paired SelfSupervisedVerifier
+    (itsd_verify_paired, verifier.py:235-240), vs the reference's outputs."""
+    g = golden("verifier_branches")
+    ov = OracleVerifier(dataset_stats={"mu": np.zeros(4), "sigma": np.eye(4)})
+    for case in ("b1", "b3", "b2_64"):
+        got = ov.score(torch.from_numpy(g[case + "_images"]).cuda())
+        assert abs(got - float(g[case + "_oracle_stats"])) <= 1e-6, case
+    sv = SelfSupervisedVerifier()
+    for case in ("p32", "p64"):
+        got = sv.score(torch.from_numpy(g[case + "_images"]).cuda(), reference_features=torch.from_numpy(g[case + "_ref"]))
+        assert abs(got - float(g[case + "_paired"])) <= 1e-6, case
+    with pytest.raises(RuntimeError):  # the reference's .item() of a 2-vector
+        sv.score(torch.zeros(2, 3, 32, 32).cuda(), reference_features=torch.zeros(2, 192))
+
+
 def test_verifier_batched_equals_per_candidate():
     gen = torch.Generator().manual_seed(9)
     im = (torch.randn(12, 3, 32, 32, generator=gen) * 0.5).clamp(-1, 1)

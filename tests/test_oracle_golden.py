@@ -158,3 +158,15 @@ def test_search_outcomes_T5():
     bn, bs, h = R.path_search(init, 3, 400, 0.1, denoise, R.oracle_score)
     np.testing.assert_allclose(np.array(h["scores"]), g["path_scores"], atol=1e-6)
     np.testing.assert_allclose(bn.numpy(), g["path_best_noise"], atol=1e-6)
+
+
+def test_verifier_branches():
+    """OracleVerifier with dataset_stats and the paired SelfSupervisedVerifier mode vs the
+    reference's own outputs (tools/gen_golden_verifier_branches.py)."""
+    g = golden("verifier_branches")
+    for case in ("b1", "b3", "b2_64"):
+        got = R.oracle_stats_score(torch.from_numpy(g[case + "_images"]))
+        assert abs(got - float(g[case + "_oracle_stats"])) <= 1e-7
+    for case in ("p32", "p64"):
+        got = R.selfsup_paired_score(torch.from_numpy(g[case + "_images"]), torch.from_numpy(g[case + "_ref"]))
+        assert abs(got - float(g[case + "_paired"])) <= 1e-7

@@ -9,6 +9,7 @@ Infinity-Cache hits are included in these memory-side counts.
 """
 import csv
 import glob
+import re
 import json
 import os
 import sys
@@ -16,8 +17,8 @@ from collections import defaultdict
 
 FAMILIES = {  # census op classes; any other argument is taken as a kernel-name substring
     "convgn": ("conv3x3_gn_kernel",),
-    "convgnw": ("conv3x3_gn_pws_kernel<32>", "conv3x3_gn_pws_kernel<16>"),
-    "convgnw4": ("conv3x3_gn_pws_kernel<8>",),
+    "convgnw": ("conv3x3_gn_p4_kernel<32>", "conv3x3_gn_p4_kernel<16>"),
+    "convgnw4": ("conv3x3_gn_p4_kernel<8>",),
     "conv": ("conv_pipe", "conv_small", "splitk_epilogue_kernel", "splitk_wide_epilogue_kernel"),
 }
 
@@ -30,7 +31,9 @@ def main():
     names = {}
     for f in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not any(p in r["Kernel_Name"] for p in pats):
+            # measurement-ablation template arguments default to 0: "<32, 0>" is the shipped "<32>"
+            kn = re.sub(r", 0>", ">", r["Kernel_Name"])
+            if not any(p in kn for p in pats):
                 continue
             k = int(r["Dispatch_Id"])
             c = r["Counter_Name"]
