@@ -195,10 +195,19 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int c = 0; c < C; c += 16) {
-        const bf16x8 af = qv ? *(const bf16x8*)(qp + c) : z8;
-        const bf16x8 bk = kv ? *(const bf16x8*)(kp + c) : z8;
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bk, acc, 0, 0, 0);
+      // q / k fragments straight from the q|k|v rows, 8 k-steps of loads in flight before
+      // their MFMAs (one dependent global round trip per 128 channels, not per 16)
+      for (int c0 = 0; c0 < C; c0 += 128) {
+        bf16x8 af[8], bk[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bool in = c0 + 16 * i < C;
+          af[i] = (qv && in) ? *(const bf16x8*)(qp + c0 + 16 * i) : z8;
+          bk[i] = (kv && in) ? *(const bf16x8*)(kp + c0 + 16 * i) : z8;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (c0 + 16 * i < C) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bk[i], acc, 0, 0, 0);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -225,27 +234,50 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
   __syncthreads();
   const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
   bf16_t* out = (bf16_t*)a.out + (size_t)img * S * C;
-  for (int t = wid; t < 2 * (C / 32); t += 4) {
-    const int ci = t >> 1, qi = t & 1;
-    const bf16_t* vp = vt + (size_t)(ci * 32 + rl) * S + 8 * hh;
-    const char* pp = Pm + (qi * 32 + rl) * PROW + 16 * hh;
-    f32x16 acc;
+  // O^T tiles (32 channels x 32 queries) t = wid + 4u: four tiles per pass with all their V^T
+  // loads of 4 k-steps in flight at once (one dependent global round trip per pass and 64 keys)
+  const int ntile = 2 * (C / 32);
+  for (int t0 = wid; t0 < ntile; t0 += 16) {
+    f32x16 acc[4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int k = 0; k < Sp; k += 16) {
-      const bf16x8 av = (k + 8 * hh < S) ? *(const bf16x8*)(vp + k) : z8;
-      const bf16x8 bp = *(const bf16x8*)(pp + 2 * k);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bp, acc, 0, 0, 0);
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+    for (int k0 = 0; k0 < Sp; k0 += 64) {
+      bf16x8 av[4][4], bp[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + 4 * u, ci = t >> 1, qi = t & 1;
+        const bool tv = t < ntile;
+        const bf16_t* vp = vt + (size_t)((tv ? ci : 0) * 32 + rl) * S + 8 * hh;
+        const char* pp = Pm + (qi * 32 + rl) * PROW + 16 * hh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + 16 * i;
+          av[u][i] = (tv && k < Sp && k + 8 * hh < S) ? *(const bf16x8*)(vp + k) : z8;
+          bp[u][i] = k < Sp ? *(const bf16x8*)(pp + 2 * k) : z8;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (t0 + 4 * u < ntile && k0 + 16 * i < Sp)
+            acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[u][i], bp[u][i], acc[u], 0, 0, 0);
     }
-    const int q = q0 + qi * 32 + rl;
-    if (q < S) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = ci * 32 + 8 * g + 4 * hh;
-        uint2 w2;
-        w2.x = (uint32_t)f2bf(acc[4 * g]) | ((uint32_t)f2bf(acc[4 * g + 1]) << 16);
-        w2.y = (uint32_t)f2bf(acc[4 * g + 2]) | ((uint32_t)f2bf(acc[4 * g + 3]) << 16);
-        *(uint2*)(out + (size_t)q * C + c) = w2;
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 4 * u, ci = t >> 1, qi = t & 1;
+      const int q = q0 + qi * 32 + rl;
+      if (t < ntile && q < S) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = ci * 32 + 8 * g + 4 * hh;
+          uint2 w2;
+          w2.x = (uint32_t)f2bf(acc[u][4 * g]) | ((uint32_t)f2bf(acc[u][4 * g + 1]) << 16);
+          w2.y = (uint32_t)f2bf(acc[u][4 * g + 2]) | ((uint32_t)f2bf(acc[u][4 * g + 3]) << 16);
+          *(uint2*)(out + (size_t)q * C + c) = w2;
+        }
       }
     }
   }
