@@ -101,6 +101,7 @@ struct Op {
   int subpix = 0;  // upsample conv as 4 phase-wise 2x2 convs (conv.hip conv_pipe)
   size_t wt = 0, bias = 0;
   size_t wfrag = SIZE_MAX;  // fragment-ordered copy of wt (fused GroupNorm convs, conv3x3_gn_reg_kernel)
+  size_t wfrag16 = SIZE_MAX;  // the same for the 16x16x32 MFMA (conv3x3_gn_p4_kernel<.., true>)
   int Cout = 0, K = 0;
   int temb_col = -1;
   int resid = -1;
@@ -258,6 +259,22 @@ struct Builder {
   }
   // [Cout][K] bf16 (k = (ky*ks+kx)*Cin + ci) -> MFMA A-fragment order [Cout/32][K/16][64][8]:
   // lane L of k-step s holds W[32*cb + (L & 31)][16*s + 8*(L >> 5) + e] (v_mfma_f32_32x32x16_bf16).
+  // A fragments of v_mfma_f32_16x16x32_bf16: lane L holds cout 16 cb + L % 16, k = 32 st + 8 (L / 16) + e
+  size_t pack_frag16(const float* Wsrc, int Cout, int Cin, int ks) {
+    const int K = ks * ks * Cin, nks = K / 32;
+    std::vector<uint16_t> b((size_t)Cout * K, 0);
+    if (Wsrc)
+      for (int cb = 0; cb < Cout / 16; ++cb)
+        for (int st = 0; st < nks; ++st)
+          for (int L = 0; L < 64; ++L)
+            for (int e = 0; e < 8; ++e) {
+              const int co = 16 * cb + (L & 15), k = 32 * st + 8 * (L >> 4) + e;
+              const int tap = k / Cin, ci = k - tap * Cin, ky = tap / ks, kx = tap - ky * ks;
+              b[(((size_t)cb * nks + st) * 64 + L) * 8 + e] =
+                  host_f2bf(Wsrc[(((size_t)co * Cin + ci) * ks + ky) * ks + kx]);
+            }
+    return ar.add(b.data(), b.size() * 2);
+  }
   size_t pack_frag(const float* Wsrc, int Cout, int Cin, int ks) {
     const int K = ks * ks * Cin, nks = K / 16;
     std::vector<uint16_t> b((size_t)Cout * K, 0);
@@ -373,6 +390,8 @@ struct Builder {
     u->ops.back().coef = coef;
     if (coef != SIZE_MAX && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
       u->ops.back().wfrag = pack_frag(W, Cout, Cin, ks);
+    if (coef != SIZE_MAX && u->bf16 && Cout % 16 == 0 && (ks * ks * Cin) % 32 == 0 && ks == 3 && Hout >= 16)
+      u->ops.back().wfrag16 = pack_frag16(W, Cout, Cin, ks);
     return dst;
   }
   // conv3x3(silu(GroupNorm(s1 ++ s2))) can run as one fused launch (conv3x3_gn_kernel)
@@ -688,6 +707,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.ksize = o.ksize; a.stride = o.stride; a.pad = o.pad; a.upsample = o.upsample;
     a.wt = u->wdev + o.wt;
     a.wfrag = o.wfrag != SIZE_MAX ? u->wdev + o.wfrag : nullptr;
+    a.wfrag16 = o.wfrag16 != SIZE_MAX ? u->wdev + o.wfrag16 : nullptr;
     a.Cout = o.Cout; a.K = o.K;
     a.bias = u->wp(o.bias);
     if (o.temb_col >= 0) {
@@ -957,6 +977,10 @@ int itsd_set_option(const char* key, int value) {
   }
   if (!std::strcmp(key, "small_korder")) {  // conv_small K order: 1 taps inside each channel chunk, 0 tap-major
     itsd::g_small_korder = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p4_m16")) {  // conv3x3_gn_p4_kernel at W = 32 / 16 on v_mfma_f32_16x16x32_bf16
+    itsd::g_p4_m16 = value ? 1 : 0;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p4_w")) {  // levels gn_reg = 4 applies to (bit 0 W = 8, 1 W = 16, 2 W = 32); others pws

@@ -13,7 +13,8 @@ extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "
 extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
 extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option "gn_reg")
 extern int g_small_korder;  // conv_small K order (itsd_set_option "small_korder")
-extern int g_p4_w;          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
+extern int g_p4_w;
+extern int g_p4_m16;        // 16x16x32 MFMA form of conv3x3_gn_p4_kernel (itsd_set_option "p4_m16")          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
 extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
@@ -91,6 +92,7 @@ struct ConvArgs {
   int zins;                          // zero-insertion (ConvTranspose2d s2 as a gather conv, ModelCondition.py:80)
   const void* wt;                    // packed [Cout][K], K = ksize*ksize*(C1+C2), k=(ky*ks+kx)*Cin+ci
   const void* wfrag;                 // the same weights in MFMA A-fragment order [Cout/32][K/16][64][8]
+  const void* wfrag16;               // ... in v_mfma_f32_16x16x32_bf16 A-fragment order [Cout/16][K/32][64][8]
                                      // (fused GroupNorm convs, bf16), or null
   int Cout, K;
   const float* bias;                 // [Cout]

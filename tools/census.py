@@ -43,7 +43,7 @@ def main():
         # each variant: '+'-joined itsd_set_option key=value pairs, e.g.
         # "base", "small_conv=0", "conv_variant=2+splitk=0", "conv_dbg=19"
         defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1, "gn_wide": 1, "conv_wide": 0,
-                    "gn_reg": 4, "small_korder": 0, "p4_w": 7}
+                    "gn_reg": 4, "small_korder": 0, "p4_w": 7, "p4_m16": 0}
         for rnd in range(3):
             for v in args.variants.split(","):
                 opts = dict(defaults)
