@@ -979,6 +979,16 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_small_korder = value ? 1 : 0;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "attn_cs")) {  // attn_mfma_kernel output-channel slices: 0 auto, 1..8 forced
+    if (value < 0 || value > 8) return fail(ITSD_ERR_INVALID, "attn_cs in [0,8]");
+    itsd::g_attn_cs = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_aq")) {  // attn_mfma_kernel queries per block: 0 auto, 32, 64
+    if (value != 0 && value != 32 && value != 64) return fail(ITSD_ERR_INVALID, "attn_aq in {0,32,64}");
+    itsd::g_attn_aq = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p4_m16")) {  // conv3x3_gn_p4_kernel at W = 32 / 16 on v_mfma_f32_16x16x32_bf16
     itsd::g_p4_m16 = value ? 1 : 0;
     return ITSD_OK;

@@ -13,6 +13,8 @@ extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "
 extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
 extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option "gn_reg")
 extern int g_small_korder;  // conv_small K order (itsd_set_option "small_korder")
+extern int g_attn_cs;       // attention output-channel slices (itsd_set_option "attn_cs")
+extern int g_attn_aq;       // attention queries per block (itsd_set_option "attn_aq")
 extern int g_p4_w;
 extern int g_p4_m16;        // 16x16x32 MFMA form of conv3x3_gn_p4_kernel (itsd_set_option "p4_m16")          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
 extern int g_num_cus;       // compute units of the device (persistent grids)

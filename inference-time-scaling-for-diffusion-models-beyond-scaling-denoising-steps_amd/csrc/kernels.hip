@@ -8,6 +8,9 @@
 
 namespace itsd {
 
+int g_attn_aq = 0;  // attn_mfma_kernel queries per block: 0 auto (32 below 512 blocks), 32, 64
+int g_attn_cs = 0;  // attn_mfma_kernel output-channel slices per block row: 0 auto, else forced
+
 // ============================================================================ GroupNorm
 // nn.GroupNorm(32, C, eps=1e-5) (Model.py:132,171,180,253) with optional Swish over
 // the channel concat of two NHWC sources (the up path's torch.cat, Model.py:280; a
@@ -170,25 +173,29 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 //  2. row softmax in fp32 over LDS, P rounded to bf16 in LDS;
 //  3. O^T = V^T P^T on MFMA with V^T channel-major (written so by the qkv conv epilogue)
 //     -> 4 consecutive channels per lane per store.
+// AQ = queries per block (64, or 32 to give small-S launches twice the blocks: at S = 64 one
+// block per image left 1 wave per SIMD, 70 % of cycles waiting on memory).
 constexpr int ATT_AQ = 64;
+template <int AQ>
 __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
+  constexpr int NQT = AQ / 32, WPQ = 4 / NQT;  // query tiles; waves per query tile in phase 1
   extern __shared__ __attribute__((aligned(16))) char asm_[];
   const int S = a.S, C = a.C, C3 = 3 * a.C;
   const int Sp = (S + 31) & ~31;
   const int SROW = Sp + 4;            // fp32 score row
   const int PROW = Sp * 2 + 16;       // bf16 P row (bytes), odd 16-B slot stride
   float* Sc = (float*)asm_;
-  char* Pm = asm_ + 64 * SROW * 4;
-  const int img = blockIdx.y, q0 = blockIdx.x * ATT_AQ;
+  char* Pm = asm_ + AQ * SROW * 4;
+  const int img = blockIdx.y, q0 = blockIdx.x * AQ;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   {
-    const int qi = wid >> 1;
+    const int qi = wid / WPQ;
     const int q = q0 + qi * 32 + rl;
     const bool qv = q < S;
     const bf16_t* qp = base + (size_t)(qv ? q : 0) * C3 + 8 * hh;
-    for (int kj = (wid & 1); kj < Sp / 32; kj += 2) {
+    for (int kj = wid % WPQ; kj < Sp / 32; kj += WPQ) {
       const int key = kj * 32 + rl;
       const bool kv = key < S;
       const bf16_t* kp = base + (size_t)(kv ? key : 0) * C3 + C + 8 * hh;
@@ -217,7 +224,7 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
     }
   }
   __syncthreads();
-  for (int r = wid * 16; r < wid * 16 + 16; ++r) {
+  for (int r = wid * (AQ / 4); r < (wid + 1) * (AQ / 4); ++r) {
     float m = -INFINITY;
     for (int j = lane; j < Sp; j += 64) m = fmaxf(m, Sc[r * SROW + j]);
     m = wave_max(m);
@@ -236,7 +243,10 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
   bf16_t* out = (bf16_t*)a.out + (size_t)img * S * C;
   // O^T tiles (32 channels x 32 queries) t = wid + 4u: four tiles per pass with all their V^T
   // loads of 4 k-steps in flight at once (one dependent global round trip per pass and 64 keys)
-  const int ntile = 2 * (C / 32);
+  // blockIdx.z splits the output channels (gridDim.z slices of C / 32 / gridDim.z channel tiles;
+  // every slice recomputes the block's scores, which are cheap next to the PV loads it spreads)
+  const int ctiles = (C / 32) / gridDim.z, cbase = blockIdx.z * ctiles;
+  const int ntile = NQT * ctiles;
   for (int t0 = wid; t0 < ntile; t0 += 16) {
     f32x16 acc[4];
 #pragma unroll
@@ -247,7 +257,7 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
       bf16x8 av[4][4], bp[4][4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int t = t0 + 4 * u, ci = t >> 1, qi = t & 1;
+        const int t = t0 + 4 * u, ci = cbase + t / NQT, qi = t % NQT;
         const bool tv = t < ntile;
         const bf16_t* vp = vt + (size_t)((tv ? ci : 0) * 32 + rl) * S + 8 * hh;
         const char* pp = Pm + (qi * 32 + rl) * PROW + 16 * hh;
@@ -267,7 +277,7 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u, ci = t >> 1, qi = t & 1;
+      const int t = t0 + 4 * u, ci = cbase + t / NQT, qi = t % NQT;
       const int q = q0 + qi * 32 + rl;
       if (t < ntile && q < S) {
 #pragma unroll
@@ -409,12 +419,21 @@ hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
       static bool attr = false;
       const size_t sm = attn_mfma_smem(a.S);
       if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)attn_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)attn_mfma_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)attn_mfma_smem(256));
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void*)attn_mfma_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)attn_mfma_smem(256));
         if (e != hipSuccess) return e;
         attr = true;
       }
-      ITSD_LAUNCH(attn_mfma_kernel, dim3((a.S + ATT_AQ - 1) / ATT_AQ, n), dim3(256), sm, s, a);
+      // output-channel slices (attn_cs): measured slower at every split (each slice repeats the
+      // score phase, which dominates: 26 -> 38 / 66 us at S = 64 for 2 / 4 slices), so 1 by default
+      const bool q32 = g_attn_aq == 32 || (g_attn_aq == 0 && (long long)n * ((a.S + 63) / 64) < 512);
+      const int cs = g_attn_cs > 0 ? g_attn_cs : 1;
+      if ((a.C / 32) % cs) return hipErrorInvalidValue;
+      if (q32) ITSD_LAUNCH(attn_mfma_kernel<32>, dim3((a.S + 31) / 32, n, cs), dim3(256), sm, s, a);
+      else ITSD_LAUNCH(attn_mfma_kernel<64>, dim3((a.S + 63) / 64, n, cs), dim3(256), sm, s, a);
       return hipGetLastError();
     }
   }

@@ -124,6 +124,14 @@ class SearchEngine:
         self._best_owner = -1
         self._ref_pending: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
+    def reserve(self, n_candidates: int, noise_shape) -> None:
+        """Size the native UNet for this rank's shard of a round up front (weights are packed
+        once per capacity; a later, larger round would otherwise re-create the handle)."""
+        _, nl = self.shard(n_candidates)
+        native = getattr(self.sampler, "_native", None)  # (sampler stand-ins in the CPU tests have none)
+        if native is not None:
+            native(nl * int(noise_shape[0]))  # the same batch sampler.run sizes the handle with
+
     def shard(self, n: int) -> Tuple[int, int]:
         if n % self.world:
             raise ValueError(f"{n} candidates do not split evenly over {self.world} ranks")
@@ -206,6 +214,7 @@ class SearchEngine:
     # --- the three searches, batched
     def random_search(self, n_candidates: int, noise_shape) -> Tuple[Optional[torch.Tensor], float, Dict[str, Any]]:
         self.best_image, self._best_owner = None, -1
+        self.reserve(n_candidates, noise_shape)
         r = self.run_round(0, n_candidates, noise_shape, kind="random")
         best_noise = None  # search_algorithm.py:60 (no candidate beat -inf)
         if r.best_index >= 0:
@@ -218,6 +227,7 @@ class SearchEngine:
                           n_iterations: int, labels=None):
         shape = tuple(initial_noise.shape)
         self.best_image, self._best_owner = None, -1
+        self.reserve(n_neighbors, shape)
         pivot = initial_noise.to(self.device, torch.float32).contiguous()
         best_noise, best_score = pivot.clone(), float("-inf")
         hist = {"scores": [], "candidates_per_iter": [], "best_index": []}
@@ -239,6 +249,7 @@ class SearchEngine:
                     labels=None):
         shape = tuple(initial_noise.shape)
         self.best_image, self._best_owner = None, -1
+        self.reserve(n_paths, shape)
         pivot = initial_noise.to(self.device, torch.float32).contiguous()
         r = self.run_round(0, n_paths, shape, pivot=pivot, scale=noise_scale, labels=labels, kind="path")
         best = pivot.clone()  # search_algorithm.py:292 (kept when no path beats -inf)

@@ -58,6 +58,9 @@ int main() {
   expect("set_option gn_reg=5", itsd_set_option("gn_reg", 5), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option gn_reg=3", itsd_set_option("gn_reg", 3), ITSD_OK);
+  expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
+  expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
+  expect("set_option p4_w=8", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it
     std::string k(4096, 'k');
@@ -134,11 +137,18 @@ int main() {
   expect("verify null scores", itsd_verify(0, f, 1, 1, 3, 32, 32, nullptr, nullptr), ITSD_ERR_INVALID);
   expect("verify n_cand=0", itsd_verify(0, f, 0, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
   expect("verify b=0", itsd_verify(0, f, 1, 0, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
-  expect("verify kind=3", itsd_verify(3, f, 1, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  expect("verify kind=4", itsd_verify(4, f, 1, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
   expect("verify kind=-1", itsd_verify(-1, f, 1, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
   expect("verify selfsup c=4", itsd_verify(1, f, 1, 2, 4, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
   expect("verify selfsup h=30", itsd_verify(1, f, 1, 2, 3, 30, 32, dd, nullptr), ITSD_ERR_INVALID);
   expect("verify selfsup b=65", itsd_verify(1, f, 1, 65, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  // ---- itsd_verify_paired
+  expect("verify_paired null images", itsd_verify_paired(nullptr, f, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  expect("verify_paired null ref", itsd_verify_paired(f, nullptr, 1, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  expect("verify_paired null scores", itsd_verify_paired(f, f, 1, 3, 32, 32, nullptr, nullptr), ITSD_ERR_INVALID);
+  expect("verify_paired n_cand=0", itsd_verify_paired(f, f, 0, 3, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  expect("verify_paired c=4", itsd_verify_paired(f, f, 1, 4, 32, 32, dd, nullptr), ITSD_ERR_INVALID);
+  expect("verify_paired w=30", itsd_verify_paired(f, f, 1, 3, 32, 30, dd, nullptr), ITSD_ERR_INVALID);
 
   // ---- itsd_attention
   expect("attention null qkv", itsd_attention(nullptr, nullptr, f, 1, 16, 64, 1, nullptr), ITSD_ERR_INVALID);
