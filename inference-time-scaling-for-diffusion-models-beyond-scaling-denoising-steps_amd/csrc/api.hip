@@ -83,6 +83,7 @@ struct Act {
   size_t off;
   int H, W, C;
   size_t stats = SIZE_MAX;  // ws offset of the channel-statistics slab (consumed by a GroupNorm), or none
+  int spi = 0;              // its slots per image (0: H*W / stat_slot_px(H*W); sub-pixel outputs: stat_spi)
 };
 
 enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF };
@@ -321,12 +322,14 @@ struct Builder {
   int upconv(int s1, const std::string& name, int Cout, int Hout) {
     const Act& A = u->acts[s1];
     const int Cin = A.C, epc = u->bf16 ? 8 : 4;
-    if ((A.H * A.W) % 128 || Cin % (8 * epc))  // sub-pixel tiles must stay inside one image
+    // sub-pixel tiles hold whole phase images or lie inside one (128-pixel tiles)
+    if (((A.H * A.W) % 128 && 128 % (A.H * A.W)) || Cin % (8 * epc))
       return conv_layer(s1, -1, name, Cout, 3, 1, 1, 1, Hout, Hout);
     const float* W = get(name + ".weight", (int64_t)Cout * Cin * 9);
     size_t wt = pack_subpix(W, Cout, Cin);
     size_t b = f32(name + ".bias", Cout);
     int dst = act(Hout, Hout, Cout);
+    if (A.H * A.W < 128) u->acts[dst].spi = 4;  // one statistics slot per (image, phase)
     conv(s1, -1, dst, wt, b, Cout, 3, 1, 1, 1);
     Op& o = u->ops.back();
     o.subpix = 1;
@@ -631,7 +634,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
       const int HW = A.H * A.W;
       if (!(128 % HW == 0 || HW % 128 == 0))
         return fail(ITSD_ERR_INVALID, "spatial size " + std::to_string(HW) + " not supported by the GN statistics slots");
-      const size_t slots = (size_t)u->nb_max * HW / stat_slot_px(HW);
+      const size_t slots = (size_t)u->nb_max * stat_spi(HW, A.spi);
       A.stats = b.ws_off;
       b.ws_off = (b.ws_off + slots * 2 * A.C * 4 + 255) & ~(size_t)255;
       bool produced = (id == u->head_out);
@@ -679,6 +682,8 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     g.eps = 1e-5f;
     g.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
     g.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    g.spi1 = u->acts[o.src1].spi;
+    g.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
     e = launch_gn_coef(g, c.nb, (float*)(u->ws + o.coef), s);
   } else if (o.kind == OP_GN) {
     GNArgs a{};
@@ -694,6 +699,8 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.dst = u->ap(o.dst);
     a.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
     a.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    a.spi1 = u->acts[o.src1].spi;
+    a.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
     e = u->bf16 ? launch_groupnorm<bf16_t>(a, c.nb, s) : launch_groupnorm<float>(a, c.nb, s);
   } else if (o.kind == OP_CONV) {
     ConvArgs a{};

@@ -128,11 +128,15 @@ struct ConvArgs {
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of
 // Gt = min(HW, 128) consecutive pixels; stats[slot][0][c] = sum, [slot][1][c] = sum of squares.
 __host__ __device__ inline int stat_slot_px(int HW) { return HW < 128 ? HW : 128; }
+// Statistics slots per image of a tensor: HW / stat_slot_px(HW), except the output of a sub-pixel
+// upsample conv whose phase images are smaller than a slot: one slot per (image, phase).
+__host__ __device__ inline int stat_spi(int HW, int spi) { return spi > 0 ? spi : HW / stat_slot_px(HW); }
 
 struct GNArgs {
   const void* src1; const void* src2;  // NHWC, C1 (+ C2) channels
   const float* st1; const float* st2;  // their statistics slabs
   int C1, C2, HW;
+  int spi1, spi2;                      // statistics slots per image of src1 / src2 (0: HW / stat_slot_px(HW))
   const float* gamma; const float* beta;
   float eps;
   int silu;

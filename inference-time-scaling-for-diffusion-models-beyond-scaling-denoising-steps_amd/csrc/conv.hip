@@ -282,7 +282,9 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
           sum += R[(g * 2) * BM + cl];
           sq += R[(g * 2 + 1) * BM + cl];
         }
-        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * (HWo / 128) + phase * (HWo / 128) + (p0 % HWo) / 128;
+        // sub-pixel phases: spp slots per phase image (one when the phase image is below a slot)
+        const int spp = HWo >= 128 ? HWo / 128 : 1;
+        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * spp + phase * spp + (p0 % HWo) / Gt;
         a.stats[(slot * 2) * a.Cout + co] = sum;
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
@@ -297,7 +299,8 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
           sum += v;
           sq = fmaf(v, v, sq);
         }
-        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * (HWo / 128) + phase * (HWo / 128) + (p0 % HWo) / 128;
+        const int spp = HWo >= 128 ? HWo / 128 : 1;
+        const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * spp + phase * spp + (p0 % HWo) / Gt;
         a.stats[(slot * 2) * a.Cout + co] = sum;
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
@@ -3435,14 +3438,18 @@ __global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
   __shared__ float gst[32][2];
   const int img = blockIdx.x, tid = threadIdx.x;
   const int C = g.C1 + g.C2, gsz = C / 32;
-  const int spi = g.HW / stat_slot_px(g.HW), n = gsz * spi;
+  const int spi1 = stat_spi(g.HW, g.spi1), spi2 = stat_spi(g.HW, g.spi2);
   {
     const int grp = tid >> 3, l8 = tid & 7;
+    // the group's (channel, slot) items: its src1 channels x spi1 slots, then src2 x spi2 (with
+    // equal slot counts the order of a single spi, c = grp*gsz + k/spi)
+    const int c0 = grp * gsz, nc1 = max(0, min(g.C1 - c0, gsz)), n1 = nc1 * spi1, n = n1 + (gsz - nc1) * spi2;
     double s = 0.0, q = 0.0;
     for (int k = l8; k < n; k += 8) {
-      const int c = grp * gsz + k / spi;
-      const long long sl = (long long)img * spi + (k % spi);
-      const bool s1 = c < g.C1;
+      const bool s1 = k < n1;
+      const int spi = s1 ? spi1 : spi2, kk = s1 ? k : k - n1;
+      const int c = c0 + (s1 ? 0 : nc1) + kk / spi;
+      const long long sl = (long long)img * spi + (kk % spi);
       const float* st = s1 ? g.st1 : g.st2;
       const int Cs = s1 ? g.C1 : g.C2, cs = s1 ? c : c - g.C1;
       s += (double)st[(sl * 2) * Cs + cs];
@@ -3747,7 +3754,8 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   const int v = g_conv_variant;
   const bool lin = !(a.upsample | a.zins);
   if (a.subpix) {
-    if (!pipe || !lin || a.ksize != 2 || (a.Hout * a.Wout) % 128) return hipErrorInvalidValue;
+    if (!pipe || !lin || a.ksize != 2 || ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
+      return hipErrorInvalidValue;
     grid.z = 4;
     ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();

@@ -26,16 +26,19 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
   __shared__ float gst[32][2];
   const int img = blockIdx.y, tid = threadIdx.x;
   const int C = a.C1 + a.C2, gs = C / 32;
-  const int Gt = stat_slot_px(a.HW), spi = a.HW / Gt;
+  const int spi1 = stat_spi(a.HW, a.spi1), spi2 = stat_spi(a.HW, a.spi2);
   {
     const int g = tid >> 3, l8 = tid & 7;
+    // the group's (channel, slot) items: its src1 channels x spi1 slots, then src2 x spi2
+    const int c0 = g * gs, nc1 = max(0, min(a.C1 - c0, gs)), n1 = nc1 * spi1, n = n1 + (gs - nc1) * spi2;
     double s = 0.0, q = 0.0;
-    for (int k = l8; k < gs * spi; k += 8) {
-      const int c = g * gs + k / spi;
-      const long long sl = (long long)img * spi + (k % spi);
-      const float* st;
-      int Cs, cc;
-      if (c < a.C1) { st = a.st1; Cs = a.C1; cc = c; } else { st = a.st2; Cs = a.C2; cc = c - a.C1; }
+    for (int k = l8; k < n; k += 8) {
+      const bool s1 = k < n1;
+      const int spi = s1 ? spi1 : spi2, kk = s1 ? k : k - n1;
+      const int c = c0 + (s1 ? 0 : nc1) + kk / spi;
+      const long long sl = (long long)img * spi + (kk % spi);
+      const float* st = s1 ? a.st1 : a.st2;
+      const int Cs = s1 ? a.C1 : a.C2, cc = s1 ? c : c - a.C1;
       s += (double)st[(sl * 2) * Cs + cc];
       q += (double)st[(sl * 2 + 1) * Cs + cc];
     }
