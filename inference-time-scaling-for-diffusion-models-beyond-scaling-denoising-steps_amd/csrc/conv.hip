@@ -3439,6 +3439,14 @@ __global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
   const int img = blockIdx.x, tid = threadIdx.x;
   const int C = g.C1 + g.C2, gsz = C / 32;
   const int spi1 = stat_spi(g.HW, g.spi1), spi2 = stat_spi(g.HW, g.spi2);
+  // gamma / beta of this thread's channels, in flight beside the statistics loads
+  float gam[8], bet[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    gam[u] = c < C ? g.gamma[c] : 0.f;
+    bet[u] = c < C ? g.beta[c] : 0.f;
+  }
   {
     const int grp = tid >> 3, l8 = tid & 7;
     // the group's (channel, slot) items: its src1 channels x spi1 slots, then src2 x spi2 (with
@@ -3470,16 +3478,21 @@ __global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
     }
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    const int grp = c / gsz;
-    const float sc = gst[grp][1] * g.gamma[c];
-    float* o = coef + ((size_t)img * (C / 8) + c / 8) * 16 + (c & 7);
-    o[0] = sc;
-    o[8] = g.beta[c] - gst[grp][0] * sc;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    if (c < C) {
+      const int grp = c / gsz;
+      const float sc = gst[grp][1] * gam[u];
+      float* o = coef + ((size_t)img * (C / 8) + c / 8) * 16 + (c & 7);
+      o[0] = sc;
+      o[8] = bet[u] - gst[grp][0] * sc;
+    }
   }
 }
 
 hipError_t launch_gn_coef(const GNArgs& g, int n, float* coef, hipStream_t s) {
+  if (g.C1 + g.C2 > 2048) return hipErrorInvalidValue;  // 8 channels per thread
   ITSD_LAUNCH(gn_coef_kernel, dim3(n), dim3(256), 0, s, g, coef);
   return hipGetLastError();
 }

@@ -27,6 +27,34 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
   const int img = blockIdx.y, tid = threadIdx.x;
   const int C = a.C1 + a.C2, gs = C / 32;
   const int spi1 = stat_spi(a.HW, a.spi1), spi2 = stat_spi(a.HW, a.spi2);
+  // loads that do not depend on the statistics are issued first (one memory round trip for
+  // the whole block instead of three): this block's 4 x 256 data chunks (host:
+  // chunks_per_block == 1024) and gamma / beta of the channels this thread finalizes
+  const unsigned cpp = C / EPC;  // chunks per pixel
+  const unsigned total = (unsigned)a.HW * cpp;
+  const unsigned c0 = blockIdx.x * (unsigned)a.chunks_per_block;
+  const unsigned c1 = min(total, c0 + (unsigned)a.chunks_per_block);
+  const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
+  const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
+  T* dst = (T*)a.dst + (size_t)img * a.HW * C;
+  u32x4 x[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const unsigned idx = c0 + u * 256 + tid;
+    x[u] = u32x4{0u, 0u, 0u, 0u};
+    if (idx < c1) {
+      const int p = (int)(idx / cpp);
+      const int c = (int)(idx - (unsigned)p * cpp) * EPC;
+      x[u] = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c) : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
+    }
+  }
+  float gam[8], bet[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    gam[u] = c < C ? a.gamma[c] : 0.f;
+    bet[u] = c < C ? a.beta[c] : 0.f;
+  }
   {
     const int g = tid >> 3, l8 = tid & 7;
     // the group's (channel, slot) items: its src1 channels x spi1 slots, then src2 x spi2
@@ -54,33 +82,19 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(GNArgs a) {
     }
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    const int g = c / gs;
-    const float sc = gst[g][1] * a.gamma[c];
-    coef[0][c] = sc;
-    coef[1][c] = a.beta[c] - gst[g][0] * sc;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    if (c < C) {
+      const int g = c / gs;
+      const float sc = gst[g][1] * gam[u];
+      coef[0][c] = sc;
+      coef[1][c] = bet[u] - gst[g][0] * sc;
+    }
   }
   __syncthreads();
-  const unsigned cpp = C / EPC;  // chunks per pixel
-  const unsigned total = (unsigned)a.HW * cpp;
-  const unsigned c0 = blockIdx.x * (unsigned)a.chunks_per_block;
-  const unsigned c1 = min(total, c0 + (unsigned)a.chunks_per_block);
-  const T* s1 = (const T*)a.src1 + (size_t)img * a.HW * a.C1;
-  const T* s2 = a.src2 ? (const T*)a.src2 + (size_t)img * a.HW * a.C2 : nullptr;
-  T* dst = (T*)a.dst + (size_t)img * a.HW * C;
-  // batches of 4 chunks per thread: all 4 loads in flight before the first use
-  for (unsigned i0 = c0; i0 < c1; i0 += 4 * 256) {
-    u32x4 x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned idx = i0 + u * 256 + tid;
-      x[u] = u32x4{0u, 0u, 0u, 0u};
-      if (idx < c1) {
-        const int p = (int)(idx / cpp);
-        const int c = (int)(idx - (unsigned)p * cpp) * EPC;
-        x[u] = c < a.C1 ? *(const u32x4*)(s1 + (size_t)p * a.C1 + c) : *(const u32x4*)(s2 + (size_t)p * a.C2 + (c - a.C1));
-      }
-    }
+  {
+    const unsigned i0 = c0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const unsigned idx = i0 + u * 256 + tid;
@@ -106,7 +120,8 @@ hipError_t launch_groupnorm(const GNArgs& a0, int n, hipStream_t s) {
   constexpr int EPC = 16 / (int)sizeof(T);
   GNArgs a = a0;
   const long long total = (long long)a.HW * ((a.C1 + a.C2) / EPC);
-  a.chunks_per_block = 1024;
+  if (a.C1 + a.C2 > 2048) return hipErrorInvalidValue;  // coefficient table / 8 channels per thread
+  a.chunks_per_block = 1024;  // = 4 chunks x 256 threads: the kernel's single batch
   const int bpi = (int)((total + a.chunks_per_block - 1) / a.chunks_per_block);
   ITSD_LAUNCH(gn_apply_kernel<T>, dim3(bpi, n), dim3(256), 0, s, a);
   return hipGetLastError();
