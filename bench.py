@@ -136,31 +136,45 @@ def kernel_file(kernel: str) -> str:
     return "".join(ch if ch.isalnum() else "_" for ch in rocprof_name(kernel)).strip("_")
 
 
+def kernel_function(kernel: str) -> str:
+    """The kernel FUNCTION of a census kernel name: template arguments dropped
+    ("conv3x3_gn_p4_kernel<32>" -> "conv3x3_gn_p4_kernel")."""
+    return rocprof_name(kernel).split("<")[0]
+
+
 def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
-    """Roofline of the conv kernel FUNCTION with the most time in the census forward."""
+    """Roofline of the conv kernel FUNCTION (all its template instantiations, e.g. the fused
+    conv at 32x32 / 16x16 / 8x8) with the most time in the census forward; the per-instantiation
+    launch counts and times are listed beside it for the rocprof cross-check."""
     per = {}
     for i, o in enumerate(ops):
         if o["kind"] in CONV_KINDS:
-            g = per.setdefault(o["kernel"] or o["kind"], [0, 0.0, 0.0, [], o["kind"]])
+            name = o["kernel"] or o["kind"]
+            g = per.setdefault(kernel_function(name), [0, 0.0, 0.0, [], o["kind"], {}])
             g[0] += 1
             g[1] += o["ms"]
             g[2] += o["flops"]
             g[3].append(i)
-    kernel = max(per, key=lambda k: per[k][1])
-    n_l, ms_census, fl_sum, idx, kind = per[kernel]
-    if steady:
-        # each launch replayed 10x back to back between HIP events (itsd_profile_op): what the
-        # replayed step graph sees, without the eager census's per-launch event overhead
-        ms_sum = sum(nat.profile_op(x, t, i, reps=10) for i in idx)
-    else:
-        ms_sum = ms_census
+            g[5].setdefault(name, []).append(i)
+    func = max(per, key=lambda k: per[k][1])
+    n_l, ms_census, fl_sum, idx, kind, inst = per[func]
+    # each launch replayed 10x back to back between HIP events (itsd_profile_op): what the
+    # replayed step graph sees, without the eager census's per-launch event overhead
+    ms_of = {i: (nat.profile_op(x, t, i, reps=10) if steady else ops[i]["ms"]) for i in idx}
+    ms_sum = sum(ms_of.values())
     achieved = fl_sum / (ms_sum * 1e-3) / 1e12
     peak = MFMA_BF16_PEAK_TFLOPS if precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
-    return kernel, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "kernel": rocprof_name(kernel),
-                    "family": KERNEL_NAMES[kind], "launches_per_forward": n_l,
-                    "avg_launch_ms": round(ms_sum / n_l, 4), "census_avg_launch_ms": round(ms_census / n_l, 4),
-                    "flops_per_launch": fl_sum / n_l}
+    insts = []
+    for name, ii in sorted(inst.items(), key=lambda kv: -sum(ms_of[i] for i in kv[1])):
+        ims = sum(ms_of[i] for i in ii)
+        ifl = sum(ops[i]["flops"] for i in ii)
+        insts.append({"kernel": rocprof_name(name), "launches_per_forward": len(ii),
+                      "avg_launch_ms": round(ims / len(ii), 4), "tflops": round(ifl / (ims * 1e-3) / 1e12, 2)})
+    return func, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                  "frac": round(achieved / peak, 4), "kernel": func,
+                  "family": KERNEL_NAMES[kind], "launches_per_forward": n_l,
+                  "avg_launch_ms": round(ms_sum / n_l, 4), "census_avg_launch_ms": round(ms_census / n_l, 4),
+                  "flops_per_launch": fl_sum / n_l, "instantiations": insts}
 
 
 def windowed_rate(smp, n: int, img: int, T: int, window: int, labels=None, rounds: int = 1):
@@ -294,23 +308,35 @@ def main():
         conv_fl = sum(v[2] for k, v in agg.items() if k in CONV_KINDS)
         # HBM traffic of the dominant kernel: PMC passes of this commit (tools/pmc_passes.sh at
         # N = 256, corrected as MI355X_MICROARCH.md prescribes), per launch
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kernel_file(kernel)}.json")
-        if os.path.exists(tfile) and args.precision == "bf16" and n_local == 256:
-            with open(tfile) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
-        dom = [o for o in ops if (o["kernel"] or o["kind"]) == kernel]
+        # (launch-weighted over the function's instantiations; null unless every one has a file)
+        traffic, tfiles = None, []
+        if args.precision == "bf16" and n_local == 256:
+            tot_b, tot_n = 0.0, 0
+            for ins in roof["instantiations"]:
+                tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kernel_file(ins['kernel'])}.json")
+                if not os.path.exists(tfile):
+                    tot_n = -1
+                    break
+                with open(tfile) as fh:
+                    tb = json.load(fh).get("hbm_bytes_per_launch")
+                ins["traffic"] = tb
+                tot_b += tb * ins["launches_per_forward"]
+                tot_n += ins["launches_per_forward"]
+                tfiles.append(os.path.relpath(tfile, ROOT))
+            if tot_n > 0:
+                traffic = tot_b / tot_n
+        dom = [o for o in ops if o["kind"] in CONV_KINDS and kernel_function(o["kernel"] or o["kind"]) == kernel]
         alg_b = sum(conv_alg_bytes(o) for o in dom) / len(dom)
         avg_s = roof["avg_launch_ms"] * 1e-3
         roof.update({
             "traffic": traffic,
-            "traffic_source": os.path.relpath(tfile, ROOT) if traffic is not None else None,
+            "traffic_source": tfiles if traffic is not None else None,
             "all_conv_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
             "conv_share_of_forward": round(conv_ms / total_ms, 4),
             "forward_ms": round(total_ms, 3),
             "forward_tflops_algorithmic": round(flops_per_image(a) * n_local / (total_ms * 1e-3) / 1e12, 2),
             # north_star: HBM GB/s of the conv tiles (dominant kernel) against the 8 TB/s peak
-            "conv_hbm": {"kernel": rocprof_name(kernel), "alg_bytes_per_launch": alg_b,
+            "conv_hbm": {"kernel": kernel, "alg_bytes_per_launch": alg_b,
                          "alg_gbps": round(alg_b / avg_s / 1e9, 1),
                          "pmc_bytes_per_launch": traffic,
                          "pmc_gbps": round(traffic / avg_s / 1e9, 1) if traffic else None,
