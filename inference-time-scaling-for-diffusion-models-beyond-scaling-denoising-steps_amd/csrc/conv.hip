@@ -3755,7 +3755,11 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
-    if (g_small_conv && conv_small_ok(a) && (g_small_conv == 2 || (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024))) {
+    // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured
+    // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt)
+    if (g_small_conv && conv_small_ok(a) &&
+        (g_small_conv == 2 ||
+         (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
       const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
       if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);
       else ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
