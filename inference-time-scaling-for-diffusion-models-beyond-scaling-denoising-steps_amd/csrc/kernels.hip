@@ -805,6 +805,7 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   bf16x8* wl = (bf16x8*)tsm;                                   // [NKS][4][3]
   char* halo = tsm + NKS * 12 * 16;                            // [(rpb+2)*(W+2)][PST]
   float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);     // [2 passes][TM_PX][3]
+  float* cfl = red + 2 * TM_PX * 3;                            // [C/8][16] this pass's GN coefficients
   for (int i = tid; i < NKS * 12; i += 256) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
   const int m = lane & 15, kg = lane >> 4;
   int hbase[2];
@@ -819,7 +820,9 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     const int im = img + pass * a.n;
     __syncthreads();
     const bf16_t* gb = (const bf16_t*)a.g + (size_t)im * HW * C;
-    const float* cf = a.coef + (size_t)im * cpp * 16;
+    // the image's GroupNorm coefficients, once in LDS
+    for (int i = tid; i < cpp * 16; i += 256) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
+    __syncthreads();
     for (int i0 = 0; i0 < total; i0 += 8 * 256) {
       u32x4 v[8];
       int dst[8];
@@ -841,14 +844,16 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
         int d = dst[u];
         if (d >= 0) {
           const int ch = (d % PST) / 16;
-          const f32x4* cp = (const f32x4*)(cf + ch * 16);
+          const f32x4* cp = (const f32x4*)(cfl + ch * 16);
           const f32x4 a0 = cp[0], a1 = cp[1], b0 = cp[2], b1 = cp[3];
+          // silu(v) = v / (1 + 2^(-v log2 e)): one exp2 and one rcp (the result is rounded to bf16)
+          auto fsilu = [](float v) { return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f)); };
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             const float x0 = __uint_as_float(v[u][w] << 16), x1 = __uint_as_float(v[u][w] & 0xffff0000u);
             const float s0 = w < 2 ? a0[2 * w] : a1[2 * w - 4], s1 = w < 2 ? a0[2 * w + 1] : a1[2 * w - 3];
             const float t0 = w < 2 ? b0[2 * w] : b1[2 * w - 4], t1 = w < 2 ? b0[2 * w + 1] : b1[2 * w - 3];
-            y[w] = (uint32_t)f2bf(silu(x0 * s0 + t0)) | ((uint32_t)f2bf(silu(x1 * s1 + t1)) << 16);
+            y[w] = pk_bf16(fsilu(x0 * s0 + t0), fsilu(x1 * s1 + t1));
           }
         } else {
           d = -2 - d;
@@ -913,7 +918,8 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
 }
 
 size_t tail_mfma_smem(int H, int W, int C) {
-  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(TM_PX / W + 2) * (W + 2) * (2 * C + 16) + 2 * TM_PX * 3 * 4;
+  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(TM_PX / W + 2) * (W + 2) * (2 * C + 16) + 2 * TM_PX * 3 * 4 +
+         (size_t)C * 2 * 4;
 }
 
 bool tail_mfma_ok(int H, int W, int C) {
