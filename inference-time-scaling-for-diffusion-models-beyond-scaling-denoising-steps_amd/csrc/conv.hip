@@ -160,9 +160,11 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
   if (a.vt_out && tileC >= a.vt_from) {
     // channel-major store of this (whole-V) tile: vt[img][c][pixel], 16-B chunks of
     // consecutive pixels of one image (host: HWo % EPC == 0, vt_from % 128 == 0); + bias only.
+    // lanes take consecutive channels (the 8 column reads of a chunk hit 64 banks once: the
+    // pixel-major order read 8 lanes per bank); each lane stores 8 consecutive pixels of its channel
     const int Cv = a.Cout - a.vt_from;
     for (int it = tid; it < BM * (BN / EPC); it += NT) {
-      const int cl = it / (BN / EPC), pl = (it - cl * (BN / EPC)) * EPC;
+      const int cl = it % BM, pl = (it / BM) * EPC;
       const int co = tileC + cl, p = tileP + pl;
       if (co >= a.Cout || p >= a.M) continue;
       const int img = p / HWo, pi = p - img * HWo;

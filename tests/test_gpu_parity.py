@@ -399,3 +399,29 @@ def test_wide_tile_convs_cfg_bit_identical():
             rt.set_option(k, v)
     assert _rel_l2(reg, outs[0]) < 1.5e-2
     assert _rel_l2(reg, torch.from_numpy(g["eps"])) < REL_L2_BF16
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_subpixel_upsample_convs_at_every_level(precision):
+    """Every nearest-x2 upsample conv of Arch A runs as 4 sub-pixel 2x2 phase GEMMs (linear
+    addressing), including the 8x8 / 16x16 outputs whose phase images are smaller than a
+    128-pixel tile: those keep one GroupNorm statistics slot per (image, phase), and the
+    following GroupNorms sum them (per-tensor slot counts). The forward stays on the oracle."""
+    a = ARCH_A
+    net = _net(a, precision)
+    n = 3
+    gen = torch.Generator().manual_seed(71)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.cuda().to(torch.int32))
+    ups = [o for o in ops if o["kind"] == "conv" and o["stride_up"] == 11]
+    assert len(ups) == 3, [o["H"] for o in ups]
+    for o in ups:  # conv_pipe<T, 2, true>: the linear (sub-pixel) variant; <.., false> is the 9-tap gather
+        assert "true" in o["kernel"], (o["H"], o["kernel"])
+    eps = net(x.cuda(), t.cuda()).cpu()
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x, t)
+    if precision == "fp32":
+        assert (eps - ref).abs().max().item() < 2e-4
+    else:
+        assert _rel_l2(eps, ref) < REL_L2_BF16
