@@ -142,6 +142,44 @@ def kernel_function(kernel: str) -> str:
     return rocprof_name(kernel).split("<")[0]
 
 
+def live_traffic(kernels, n: int, timeout_s: float = 150.0):
+    """HBM bytes per launch of each kernel instantiation, measured in THIS run: two rocprofv3
+    --pmc passes (FETCH_SIZE, then WRITE_SIZE: separate runs, no tracing domains) over one census
+    forward in a child process, reduced by tools/pmc_traffic.py (FETCH_SIZE x 2 on gfx950 +
+    WRITE_SIZE). Returns {kernel: bytes} or None when the profiler is unavailable or fails."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    env = dict(os.environ, TMPDIR="/tmp")
+    d = tempfile.mkdtemp(prefix="itsd_pmc_", dir="/tmp")
+    try:
+        for i, ctr in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", os.path.join(d, f"p{i}"), "-o", "run", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "census.py"), "--reps", "1", "--n", str(n)]
+            r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout_s)
+            if r.returncode != 0:
+                return None
+        out = {}
+        for k in kernels:
+            js = os.path.join(d, "t.json")
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), d, k, js], cwd=ROOT,
+                               capture_output=True, text=True, timeout=60)
+            if r.returncode != 0 or not os.path.exists(js):
+                return None
+            with open(js) as fh:
+                out[k] = json.load(fh)["hbm_bytes_per_launch"]
+            os.remove(js)
+        return out
+    except Exception:
+        return None
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
     """Roofline of the conv kernel FUNCTION (all its template instantiations, e.g. the fused
     conv at 32x32 / 16x16 / 8x8) with the most time in the census forward; the per-instantiation
@@ -243,6 +281,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip sweep / fp32 / legs")
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="take the dominant kernel's HBM traffic from profiles/ instead of two PMC passes")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -308,9 +348,22 @@ def main():
         conv_fl = sum(v[2] for k, v in agg.items() if k in CONV_KINDS)
         # HBM traffic of the dominant kernel: PMC passes of this commit (tools/pmc_passes.sh at
         # N = 256, corrected as MI355X_MICROARCH.md prescribes), per launch
-        # (launch-weighted over the function's instantiations; null unless every one has a file)
+        # (launch-weighted over the function's instantiations): measured live in this run by two
+        # PMC passes of a child process; else (profiler unavailable) from this commit's committed
+        # PMC files at N = 256; null unless every instantiation has a number
         traffic, tfiles = None, []
-        if args.precision == "bf16" and n_local == 256:
+        live = None
+        if args.precision == "bf16" and not args.no_live_traffic and world == 1:
+            progress("PMC traffic passes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, child process)")
+            live = live_traffic([ins["kernel"] for ins in roof["instantiations"]], n_local)
+        if live is not None:
+            tot_b = sum(live[ins["kernel"]] * ins["launches_per_forward"] for ins in roof["instantiations"])
+            tot_n = sum(ins["launches_per_forward"] for ins in roof["instantiations"])
+            for ins in roof["instantiations"]:
+                ins["traffic"] = live[ins["kernel"]]
+            traffic = tot_b / tot_n
+            tfiles = "live: rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in this run"
+        elif args.precision == "bf16" and n_local == 256:
             tot_b, tot_n = 0.0, 0
             for ins in roof["instantiations"]:
                 tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{kernel_file(ins['kernel'])}.json")
