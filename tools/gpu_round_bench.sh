@@ -16,6 +16,6 @@ done
 timeout -k 10 600 python bench.py > gpurun_out/$R/bench.json 2> gpurun_out/$R/bench.err || { echo bench_fail; tail -5 gpurun_out/$R/bench.err; exit 1; }
 tail -c 600 gpurun_out/$R/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$R/prof -o bench -- python3 bench.py --no-extras --no-cpu-baseline > gpurun_out/$R/prof_bench.json 2> gpurun_out/$R/prof.err || { echo prof_fail; tail -5 gpurun_out/$R/prof.err; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$R/prof -o bench -- python3 bench.py --no-extras --no-cpu-baseline --no-live-traffic > gpurun_out/$R/prof_bench.json 2> gpurun_out/$R/prof.err || { echo prof_fail; tail -5 gpurun_out/$R/prof.err; exit 1; }
 find gpurun_out/$R/prof -name "*kernel_trace.csv" -delete
 find gpurun_out/$R/prof -name "*stats.csv" | head
