@@ -425,3 +425,21 @@ def test_subpixel_upsample_convs_at_every_level(precision):
         assert (eps - ref).abs().max().item() < 2e-4
     else:
         assert _rel_l2(eps, ref) < REL_L2_BF16
+
+
+def test_forward_bf16_full_batch_vs_oracle_subset():
+    """The bench batch (N=256) runs the persistent fused convs with several tiles per block
+    (4 at 32x32, 2 at 16x16), the 2-blocks-per-image attention grid and the split-K small level: images
+    spread over the batch match the oracle (fp32, CPU) within the bf16 bound."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    n = 256
+    gen = torch.Generator().manual_seed(256)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    eps = net(x.cuda(), t.cuda()).float().cpu()
+    idx = torch.tensor([0, 1, 63, 128, 200, 255])
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    for k, i in enumerate(idx.tolist()):
+        assert _rel_l2(eps[i], ref[k]) < REL_L2_BF16, (i, _rel_l2(eps[i], ref[k]))
