@@ -18,6 +18,6 @@ for f in conv kernels; do
 done
 wait
 $HIPCC -O1 -g -std=c++17 $SAN -I include -c tests/asan/abi_validation.cpp -o $OUT/abi_validation.o
-$HIPCC --offload-arch=gfx950 -fsanitize=address -o $OUT/abi_validation $OUT/abi_validation.o $OUT/api_asan.o \
+$HIPCC --offload-arch=gfx950 -fsanitize=address -fno-gpu-sanitize -o $OUT/abi_validation $OUT/abi_validation.o $OUT/api_asan.o \
   $OUT/conv.o $OUT/kernels.o
 echo $OUT/abi_validation
