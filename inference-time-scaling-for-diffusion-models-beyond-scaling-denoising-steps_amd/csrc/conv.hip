@@ -3405,10 +3405,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     }
     const bool res = RES && a.resid && cc == ncc - 1;
     if (res) res_dma(k);
-    if (q + 1 < nstages) {
-      if (cc == ncc - 1) stage_addv(k + 1, tt);
-      emit(smem + ((q + 1) & 1) * HALO);
-    }
+    // tile k+1's addv: RES tiles seed their accumulators from it after tile k (its other parity
+    // was last read when tile k-1 started), so it is staged with tile k's FIRST chunk, away from
+    // the last chunk's residual DMA and drain (at two chunks per tile that stage carried them all);
+    // the register epilogue (8x8) still reads parity k+1 = k-1 during chunk 0, so it waits for the last
+    const int addv_cc = RES ? 0 : ncc - 1;
+    if (cc == addv_cc && k + 1 < ntiles) stage_addv(k + 1, tt);
+    if (q + 1 < nstages) emit(smem + ((q + 1) & 1) * HALO);
     // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
     // issued after it, may still be in flight)
     if (res) {  // (last stage: nothing was issued after the DMA)
