@@ -1,5 +1,12 @@
 """End-to-end eval entry points on the GPU (Main.py / MainCondition.py surface) with tiny
-UNets loaded from reference-format checkpoint files."""
+UNets loaded from reference-format checkpoint files.
+
+What these tests pin: the entry's plumbing (config keys, checkpoint loading with the `module.`
+prefix, seeds, the x_T draw, the sampler call, the PNG grid layout) against a hand-run of the
+same itsd components, i.e. the entry against itself. The numerics underneath are pinned
+elsewhere (tests/test_gpu_parity.py vs the reference's fixtures). The PNG bytes are
+parity-unpinned: torchvision (the reference's save_image) is not installed here, so the grid is
+compared with the repo's own torchvision-compatible make_grid."""
 import dataclasses
 import os
 
