@@ -4,23 +4,25 @@ One "step" = one RandomSearch round: N_local candidates per GPU x T=1000 DDPM st
 of the CIFAR-10 32x32 UNet (Arch A, config/config.yaml:25-29) in bf16 on MI355X,
 the Oracle verifier on every candidate, one all_gather of the scores, argmax.
 Weights: the seeded non-degenerate synthetic recipe (no checkpoint offline);
-noise: Philox. Weak scaling by default (every GPU owns N_local candidates);
---n-total N fixes the global N instead (strong scaling).
+noise: Philox. The metric's N = 256 candidates per round are split over the GPUs (strong
+scaling, N_local = 256 / n_gpus); --n-per-gpu N runs N per GPU instead (weak scaling), and a
+multi-GPU run also reports the N = 256-per-GPU weak-scaling rate as a side field.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-total N] [--no-extras]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n N | --n-per-gpu N] [--no-extras]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
 Rank 0 prints ONE JSON line. Extra fields (single-GPU runs):
   roofline      the dominant kernel (fused GroupNorm conv) in steady state with HIP events on
                 the UNet's stream, its PMC HBM traffic (profiles/, this commit), the conv tiles'
                 HBM GB/s, and the attention kernels' MFMA utilisation;
-  sweep         N in {64, 1024} (north_star), same path;
+  sweep         N in {32, 64, 256, 1024} on one GPU (north_star's N set; N = 32 is the 8-GPU
+                shard of N = 256), same path;
   fp32          the reference-precision (parity mode) throughput at the headline N;
   legs          the other BASELINE configs per GPU shard: C3 CFG zero-order round (Arch C,
                 N_local = 32 -> 2N = 64 guided batch), C4 64x64 Arch A (N_local = 16), C5
                 T = 3000 path search (N_local = 128), each with its own dominant kernel;
   cpu_baseline  the CPU oracle (fp32) timed on this host's cores at B in {1, 8, 32} plus a
-                short full-loop conversion check.
+                full-loop conversion check (equal interleaved windows, `agrees` within 15 %).
 Windowed lines time a contiguous window of sampler steps (every DDPM step runs the same
 UNet, so candidate-images/s at T = N / (T x per-step time)); the window is stated in each.
 """
@@ -52,11 +54,15 @@ KERNEL_NAMES = {  # op classes of the census
 }
 
 
-def cpu_baseline(T: int, seconds: float = 15.0):
+def cpu_baseline(T: int, seconds: float = 12.0, check_seconds: float = 10.0):
     """Reference-equivalent CPU sampler (oracle, fp32) on this host's cores: UNet forwards of
-    Arch A at B in {1, 8, 32} (about seconds/3 each), converted to candidate-images/s at T
-    (img-fwd/s / T; the sampler update is negligible next to the forward), plus one full
-    N = 1 p_sample loop over a short T (the conversion check)."""
+    Arch A at B in {1, 8, 32} (seconds/3 each), converted to candidate-images/s at T
+    (img-fwd/s / T; the sampler update is negligible next to the forward).
+
+    Conversion check: the full N = 1 ancestral loop (R.p_sample_loop, short T) and B = 1
+    forwards, each timed over an equal window of check_seconds, interleaved twice (loop,
+    forwards, loop, forwards) so that host-frequency drift or a neighbour's load hits both
+    legs alike; the best of each is compared and `agrees` is true within +-15 %."""
     from oracle import ref_cpu as R
     from itsd.arch import ARCH_A
     from itsd.weights import synthetic_state_dict
@@ -67,34 +73,46 @@ def cpu_baseline(T: int, seconds: float = 15.0):
     a = ARCH_A
     sd = synthetic_state_dict(a, 0)
     fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
-    sch = R.schedule(1e-4, 0.02, T)
+
+    def fwd_rate(b, window):
+        x = torch.randn(b, 3, 32, 32)
+        t = torch.full((b,), 500, dtype=torch.long)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < window or n == 0:
+            fw(x, t)
+            n += 1
+        return n * b / (time.perf_counter() - t0)
+
+    def loop_rate(window):
+        Tc = 10
+        sc = R.schedule(1e-4, 0.02, Tc)
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < window or steps == 0:
+            R.p_sample_loop(fw, torch.randn(1, 3, 32, 32), sc, lambda s, xx: torch.randn_like(xx))
+            steps += Tc
+        return steps / (time.perf_counter() - t0)
+
     per_b = {}
     with torch.no_grad():
+        fwd_rate(1, 0.5)  # warm the thread pool and the allocator
         for b in (1, 8, 32):
-            x = torch.randn(b, 3, 32, 32)
-            t = torch.full((b,), 500, dtype=torch.long)
-            fw(x, t)  # warm
-            n, t0 = 0, time.perf_counter()
-            while time.perf_counter() - t0 < seconds / 3 or n == 0:
-                fw(x, t)
-                n += 1
-            dt = time.perf_counter() - t0
-            per_b[b] = n * b / dt
-        # conversion check: a full N = 1 ancestral loop over Tc steps
-        Tc = 20
-        sc = R.schedule(1e-4, 0.02, Tc)
-        x = torch.randn(1, 3, 32, 32)
-        t0 = time.perf_counter()
-        R.p_sample_loop(fw, x, sc, lambda s, xx: torch.randn_like(xx))
-        dtc = time.perf_counter() - t0
+            per_b[b] = fwd_rate(b, seconds / 3)
+        loops, fwds = [], []
+        for _ in range(2):
+            loops.append(loop_rate(check_seconds / 2))
+            fwds.append(fwd_rate(1, check_seconds / 2))
     best_b = max(per_b, key=per_b.get)
+    lr, fr = max(loops), max(fwds)
+    dev = (lr - fr) / fr
     return {"value": per_b[best_b] / T, "unit": "candidate-images/sec", "cores": cores, "kind": "port",
             "sample": f"Arch A fp32 UNet forwards at B=1/8/32: {per_b[1]:.2f}/{per_b[8]:.2f}/{per_b[32]:.2f} "
                       f"img-fwd/s ({seconds / 3:.0f}s each), value = best (B={best_b}) / T={T}; "
-                      f"check: full N=1 loop of {Tc} steps {dtc:.2f}s = {Tc / dtc:.2f} steps/s vs "
-                      f"{per_b[1]:.2f} img-fwd/s at B=1",
+                      f"check: full N=1 loop {lr:.2f} steps/s vs B=1 forwards {fr:.2f} img-fwd/s "
+                      f"({check_seconds:.0f}s each, interleaved)",
             "img_fwd_per_s": {str(k): round(v, 3) for k, v in per_b.items()},
-            "full_loop_check": {"T": Tc, "N": 1, "seconds": round(dtc, 3), "steps_per_s": round(Tc / dtc, 3)}}
+            "full_loop_check": {"N": 1, "window_s": check_seconds, "loop_steps_per_s": [round(v, 3) for v in loops],
+                                "b1_fwd_per_s": [round(v, 3) for v in fwds], "deviation": round(dev, 4),
+                                "agrees": abs(dev) <= 0.15}}
 
 
 def census(net, n: int, img: int, labels=None):
@@ -274,8 +292,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n-per-gpu", type=int, default=256)
-    ap.add_argument("--n-total", type=int, default=0, help="strong scaling: fixed global N split over the GPUs")
+    ap.add_argument("--n", "--n-total", dest="n_total", type=int, default=256,
+                    help="global N of the metric (N=256), split over the GPUs: strong scaling (default)")
+    ap.add_argument("--n-per-gpu", type=int, default=0, help="weak scaling instead: N per GPU")
     ap.add_argument("--T", type=int, default=1000)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
@@ -283,7 +302,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip sweep / fp32 / legs")
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="take the dominant kernel's HBM traffic from profiles/ instead of two PMC passes")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-weak-line", action="store_true", help="(N > 1) skip the N=256-per-GPU weak-scaling field")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -291,7 +311,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under torchrun (any world size, 1 included) the ranks form an RCCL group and the round
+    # protocol runs its collectives; a plain `python bench.py` runs without one
+    use_pg = "WORLD_SIZE" in os.environ and "MASTER_ADDR" in os.environ
+    if use_pg:
         dist.init_process_group("nccl", device_id=dev)
 
     import itsd
@@ -302,13 +325,13 @@ def main():
     from itsd.verifier import OracleVerifier
 
     a = ARCH_A
-    if args.n_total:
-        if args.n_total % world:
-            raise SystemExit(f"--n-total {args.n_total} does not split over {world} GPUs")
-        n_total, n_local, scaling = args.n_total, args.n_total // world, "strong"
-    else:
+    if args.n_per_gpu:
         n_local, scaling = args.n_per_gpu, "weak"
         n_total = n_local * world
+    else:  # the metric's N = 256 candidates per round, split over the GPUs
+        if args.n_total % world:
+            raise SystemExit(f"--n {args.n_total} does not split over {world} GPUs")
+        n_total, n_local, scaling = args.n_total, args.n_total // world, "strong"
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision=args.precision,
                weights="gauss", seed=0, device=dev)
     smp = GaussianDiffusionSampler(net, 1e-4, 0.02, args.T)
@@ -321,7 +344,7 @@ def main():
     for w in range(args.warmup):
         eng.run_round(10_000 + w, n_total, shape)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     t0 = time.perf_counter()
     best = None
@@ -329,13 +352,33 @@ def main():
         r = eng.run_round(k, n_total, shape)
         best = (r.best_index, r.best_score)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if use_pg:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+
+    # N > 1 with the metric's fixed N = 256: also the weak-scaling rate (N = 256 per GPU, the same
+    # round protocol over the same ranks) as a side field; the headline stays the metric's N
+    weak = None
+    if world > 1 and scaling == "strong" and not args.no_weak_line:
+        nw = 256 * world
+        net.reserve(256)
+        eng.run_round(20_000, nw, shape)  # capture the N_local = 256 graph
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for k in range(args.steps):
+            eng.run_round(30_000 + k, nw, shape)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tw = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        weak = {"value": round(nw * args.steps / float(tw.item()), 3), "unit": "candidate-images/sec",
+                "global_batch": nw, "n_local": 256, "steps": args.steps, "scaling": "weak",
+                "ms_per_step": round(float(tw.item()) / args.steps * 1e3, 2)}
 
     roof = None
     if rank == 0:
@@ -409,7 +452,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         # north_star N sweep on the same path (headline N is the main line)
         sweep = {}
-        for n, window in ((64, 1000), (1024, 100)):
+        for n, window in ((32, 1000), (64, 1000), (256, 1000), (1024, 100)):
             if n == n_local:
                 continue
             progress(f"sweep N={n}")
@@ -463,12 +506,15 @@ def main():
                                    f"Arch A UNet 32x32 (ch128 [1,2,3,4] attn[2] nrb2), Oracle verifier",
                        "model": "DDPM UNet (Diffusion/Model.py) Arch A", "global_batch": n_total, "seq_len": args.T,
                        "parallelism": f"candidate-dp{world}", "T": args.T, "graph": not args.no_graph,
+                       "process_group": dist.get_backend() if use_pg else None, "n_local": n_local,
                        "best_candidate": best},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if weak is not None:
+            out["weak_scaling"] = weak
         out.update(extras)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

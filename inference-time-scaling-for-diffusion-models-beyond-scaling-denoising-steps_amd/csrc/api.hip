@@ -14,6 +14,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -912,7 +913,11 @@ int check_batch(itsd_unet* u, int n) {
 
 // ============================================================================ C ABI
 namespace itsd {
-const char* g_last_kernel = nullptr;
+thread_local const char* g_last_kernel = nullptr;
+std::mutex& kernel_names_mu() {
+  static std::mutex m;
+  return m;
+}
 std::vector<const char*>& kernel_names() {
   static std::vector<const char*> v;
   return v;
@@ -921,6 +926,7 @@ std::vector<const char*>& kernel_names() {
 // the ITSD_LAUNCH string literals, so equal sites compare equal by content)
 int kernel_id(const char* name) {
   if (!name) return 0;
+  std::lock_guard<std::mutex> lk(kernel_names_mu());
   auto& v = kernel_names();
   for (size_t i = 0; i < v.size(); ++i)
     if (v[i] == name || !std::strcmp(v[i], name)) return (int)i + 1;
@@ -934,6 +940,7 @@ extern "C" {
 int itsd_version(void) { return 1; }
 
 const char* itsd_kernel_name(int id) {
+  std::lock_guard<std::mutex> lk(itsd::kernel_names_mu());
   return id > 0 && id <= (int)itsd::kernel_names().size() ? itsd::kernel_names()[id - 1] : "";
 }
 

@@ -23,7 +23,9 @@ extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_s
 // Census (itsd_profile_ops): the first kernel an op launches. Every launch site goes through
 // ITSD_LAUNCH, which records the kernel expression's name if none is recorded yet; the census
 // clears it before each op and maps the name to a small id (kernel_id, itsd_kernel_name).
-extern const char* g_last_kernel;
+// Per thread (a census on one thread never reads another thread's launches); kernel_id's
+// registry is guarded by a mutex.
+extern thread_local const char* g_last_kernel;
 int kernel_id(const char* name);
 #define ITSD_LAUNCH(K, ...)                                    \
   do {                                                         \

@@ -229,7 +229,8 @@ def _device(cfg: Dict[str, Any]) -> torch.device:
     """``device`` (``Train.py:811``) and the inference config's ``device_ids`` /
     ``use_multi_gpu`` (``abstract_metrics_from_pretrained_ddpm.py:52-123``). itsd runs one
     process per GPU (torchrun) instead of DataParallel: under torchrun rank r takes
-    ``device_ids[LOCAL_RANK]`` (or ``cuda:LOCAL_RANK``); one process takes ``device_ids[0]``."""
+    ``device_ids[LOCAL_RANK]``, else ``cuda:(i + LOCAL_RANK)`` for ``device: cuda:i`` (``cuda``:
+    i = 0) -- never one GPU for every rank; one process takes ``device_ids[0]`` / ``cuda:i``."""
     spec = str(cfg.get("device") or "cuda")
     if spec.split(":")[0] != "cuda":
         raise ValueError("itsd samples on the GPU only; set device: cuda")
@@ -245,6 +246,8 @@ def _device(cfg: Dict[str, Any]) -> torch.device:
             raise ValueError(f"device_ids {list(ids)} has no entry for LOCAL_RANK {local}")
         return torch.device("cuda", int(ids[local if world > 1 else 0]))
     dev = torch.device(spec.split(",")[0])
+    if world > 1:  # one GPU per rank: the configured index is the first rank's
+        return torch.device("cuda", (dev.index or 0) + local)
     if dev.index is None:
         dev = torch.device("cuda", local if "LOCAL_RANK" in os.environ else torch.cuda.current_device())
     return dev
@@ -430,14 +433,18 @@ def _out_dir(cfg: Dict[str, Any]) -> str:
 
 def _sample_sharded(sampler, noisy: torch.Tensor, labels: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``sampler(noisy[, labels])`` with the batch split over the ranks of a torchrun job:
-    every rank holds the same x_T draw (same seed), runs its contiguous slice with the
-    Philox noise of the slice's global image indices, and rank 0 gathers the result --
-    bit-identical to the single-process run. One process: a plain sampler call."""
+    rank 0's x_T (and labels) are broadcast, every rank runs its contiguous slice with the
+    Philox noise of the slice's global image indices, and the result is gathered --
+    bit-identical to the single-process run. One process: a plain sampler call.
+    ``noisy`` / ``labels`` are overwritten in place with rank 0's values."""
     rank, world = _rank_world()
     if world == 1 or noisy.shape[0] % world:
         return sampler(noisy) if labels is None else sampler(noisy, labels)
     seed = torch.tensor([int(torch.randint(0, 2 ** 62, (1,)).item())], dtype=torch.int64, device=noisy.device)
     torch.distributed.broadcast(seed, src=0)  # one sampler seed even if the ranks' generators differ
+    torch.distributed.broadcast(noisy, src=0)  # ADVICE r2: the saved noisy grid is what every rank slices
+    if labels is not None:
+        torch.distributed.broadcast(labels, src=0)
     nl = noisy.shape[0] // world
     per = noisy[0].numel()
     x = noisy[rank * nl:(rank + 1) * nl].clone().contiguous()

@@ -23,7 +23,8 @@ Two layers:
    exactly the order the reference's sequential loops consume them, and feeds them
    to the batched sampler as injected noise -- the batched search then reproduces
    the reference's scores, argmax and best noise bit for bit under
-   ``torch.manual_seed``.
+   ``torch.manual_seed`` -- of a reference run with ``device="cpu"`` (its default
+   ``device="cuda"`` would draw from the CUDA generator); small rounds only.
 """
 from __future__ import annotations
 
@@ -70,7 +71,14 @@ class ReferenceNoise:
       ``pivot + randn_like(pivot) * (1 - lambda)`` first, then per neighbour T-1 draws;
     * path (``:305-318``): per path ``initial + randn_like(initial) * scale``, then T-1.
 
-    Returns (x_T [n*B,...], noise [T, n*B, ...]) on the CPU; noise[t] feeds step t."""
+    Returns (x_T [n*B,...], noise [T, n*B, ...]) on the CPU; noise[t] feeds step t.
+
+    Parity is defined against a reference run with ``device="cpu"`` (what search_T5.npz
+    holds): the reference's default ``device="cuda"`` draws from the CUDA generator instead.
+    The whole [T, n*B, ...] plan is materialised on the host and copied to the device, so it
+    is meant for parity-sized rounds: above ``MAX_ELEMENTS`` it refuses (use Philox mode)."""
+
+    MAX_ELEMENTS = 1 << 28  # 1 GiB of fp32 noise per round
 
     def __init__(self, T: int):
         self.T = int(T)
@@ -81,6 +89,10 @@ class ReferenceNoise:
 
     def round(self, kind: str, n: int, shape, pivot: Optional[torch.Tensor] = None, scale: float = 1.0):
         shape = tuple(shape)
+        total = self.T * n * int(torch.Size(shape).numel())
+        if total > self.MAX_ELEMENTS:
+            raise ValueError(f"reference-order noise plan of {total} elements (T={self.T}, n={n}) exceeds "
+                             f"{self.MAX_ELEMENTS}: parity mode is for small rounds, use noise='philox'")
         xs, zs = [], []
         if kind == "zero_order":
             p = pivot.detach().cpu().float()
@@ -113,8 +125,11 @@ class SearchEngine:
         self.seed = int(seed)
         self.group = group
         self.graph = graph
-        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        # with a process group (even of one rank) the round protocol runs its collectives: the
+        # code path of an N-GPU job is the one a 1-GPU job under torchrun executes
+        self.dist = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.rank = dist.get_rank(group) if self.dist else 0
         if noise == "reference" and self.world > 1:
             raise ValueError("noise='reference' follows one process's global generator; use 'philox' when sharded")
         self.noise = noise
@@ -174,7 +189,7 @@ class SearchEngine:
                              noise_offset=g0 * per, graph=self.graph)
         local = self.verifier.score_batch(x, nl)
         self.nfes += n
-        if self.world > 1:
+        if self.dist:
             parts = [torch.empty_like(local) for _ in range(self.world)]
             dist.all_gather(parts, local.contiguous(), group=self.group)  # the round's one collective
             scores = torch.cat(parts)
@@ -205,11 +220,13 @@ class SearchEngine:
             self.best_image = None
 
     def _publish_best_image(self, shape) -> None:
-        """One broadcast from the owner at the end of the search (world > 1)."""
-        if self.world > 1 and self._best_owner >= 0:
+        """One broadcast from the owner at the end of the search (under a process group)."""
+        if self.dist and self._best_owner >= 0:
             if self.best_image is None:
                 self.best_image = torch.empty(tuple(shape), dtype=torch.float32, device=self.device)
-            dist.broadcast(self.best_image, src=self._best_owner, group=self.group)
+            # the owner is a rank of self.group; broadcast's src is a global rank
+            src = self._best_owner if self.group is None else dist.get_global_rank(self.group, self._best_owner)
+            dist.broadcast(self.best_image, src=src, group=self.group)
 
     # --- the three searches, batched
     def random_search(self, n_candidates: int, noise_shape) -> Tuple[Optional[torch.Tensor], float, Dict[str, Any]]:

@@ -52,3 +52,15 @@ def test_pmc_traffic_reduction(tmp_path):
     # per launch: mean over the two dispatches of (FETCH x 2 + WRITE), KiB -> bytes
     want = ((100 * 2 + 40) + (120 * 2 + 60)) / 2 * 1024
     assert abs(t["hbm_bytes_per_launch"] - want) < 1e-6
+
+
+def test_cpu_baseline_conversion_check_fields():
+    """The CPU baseline's conversion check is a check: equal interleaved windows of the full N = 1
+    loop and of B = 1 forwards, a deviation, and `agrees` within +-15 % (tiny windows here)."""
+    b = _bench()
+    r = b.cpu_baseline(1000, seconds=0.6, check_seconds=0.8)
+    c = r["full_loop_check"]
+    assert r["kind"] == "port" and r["cores"] >= 1 and r["value"] > 0
+    assert len(c["loop_steps_per_s"]) == 2 and len(c["b1_fwd_per_s"]) == 2
+    dev = (max(c["loop_steps_per_s"]) - max(c["b1_fwd_per_s"])) / max(c["b1_fwd_per_s"])
+    assert abs(c["deviation"] - dev) < 1e-3 and c["agrees"] == (abs(c["deviation"]) <= 0.15)
