@@ -976,16 +976,30 @@ int itsd_set_option(const char* key, int value) {
     // 4096 | (mask << 13): compile-time ablations of conv3x3_gn_reg_kernel<32> (conv.hip)
     // (1 << 20) / (1 << 21): s_setprio 1 / 2 for the halo waves of the ws / pws fused GroupNorm convs
     itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13) | (3 << 20));
+#ifndef ITSD_DIAG
+    if (itsd::g_conv_dbg & 4096) {
+      itsd::g_conv_dbg = 0;
+      return fail(ITSD_ERR_INVALID, "conv_dbg 4096 (compile-time ablations): diagnostic builds only (tools/build_diag.sh)");
+    }
+#endif
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {
-    // 256-pixel conv tiles (conv3x3_gn_wide_kernel / conv_pipe_wide): 0 off, 1 auto, 2 whenever eligible
+    // 256-pixel conv tiles (gn_wide: the persistent conv3x3_gn_p4_kernel; conv_wide: conv_pipe_wide,
+    // diagnostic builds only): 0 off, 1 auto, 2 whenever eligible
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, std::string(key) + " in [0,2]");
+#ifndef ITSD_DIAG
+    if (key[0] == 'c' && value) return fail(ITSD_ERR_INVALID, "conv_wide: diagnostic builds only (tools/build_diag.sh)");
+#endif
     (key[0] == 'g' ? itsd::g_gn_wide : itsd::g_conv_wide) = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_reg")) {
+    // 4: conv3x3_gn_p4_kernel (shipped); 0-3: the superseded 256-pixel kernels, diagnostic builds only
     if (value < 0 || value > 4) return fail(ITSD_ERR_INVALID, "gn_reg in [0,4]");
+#ifndef ITSD_DIAG
+    if (value != 4) return fail(ITSD_ERR_INVALID, "gn_reg 0-3 (superseded 256-pixel kernels): diagnostic builds only");
+#endif
     itsd::g_gn_reg = value;
     return ITSD_OK;
   }

@@ -1003,15 +1003,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_kernel(ConvArgs a) {
   conv_epilogue<T>(a, acc, smem, tileP, tileC);
 }
 
-// ---------------------------------------------------------------------------- 256-pixel tiles
-// The census of the 128 x 128 kernels with their measurement switches (itsd_set_option
-// "conv_dbg") showed their loops bound by the per-stage operand stream and its latency, not
-// by the matrix pipe: with the MFMAs skipped, conv3x3_gn_kernel still took 62 % of its time.
-// The kernels below take a 128 couts x 256 pixels tile with 8 waves (2 cout halves x 4 pixel
-// quarters of 64 x 64) sharing every stage -- twice the MFMAs per streamed weight byte -- and
-// one block owns the CU's 160 KiB of LDS, so the ring keeps more stages in flight. Per output,
-// the MFMA sequence (tap, channel chunk, k) and the epilogue are the 128-pixel kernels', so
-// without a K split the results are bit-identical to theirs.
+// ---------------------------------------------------------------------------- 256-pixel tiles (persistent)
 #ifdef ITSD_STAMPS
 // Diagnostic build only (hipcc -DITSD_STAMPS): per-wave cycle shares of the wide fused conv's
 // phases, [block % 1024][wave][phase] (the last launch to touch a slot wins). Never shipped.
@@ -1033,635 +1025,7 @@ constexpr int GNW_EPI = GNW_BN * EROW * 4 + (GNW_BN / 16) * 2 * CONV_BM * 4;  //
 constexpr int GNW_SMEM = 160 * 1024;
 static_assert(GNW_EPI <= GNW_SMEM, "epilogue tile");
 
-// accumulators of the 8 waves (2 x 4 of 64 x 64) -> E[pixel][cout] (256 x 128 fp32)
-__device__ __forceinline__ void acc_to_E_wide(f32x16 (&acc)[2][2], float* E) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 v4 = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-        *(f32x4*)(E + (wn * 64 + j * 32 + rl) * EROW + wm * 64 + i * 32 + 8 * g + 4 * hh) = v4;
-      }
-}
-
-// Fused GroupNorm+SiLU+conv3x3 (conv3x3_gn_kernel's work, Model.py:170-174,179-184) at 256
-// pixels: 8 rows of a 32x32 image or a whole 16x16 image (NSEG = 1), four 8x8 images (NSEG = 4).
-//   * weight ring NS deep: NS-1 stages in flight across the raw barriers;
-//   * double-buffered halo: the next chunk's GroupNorm+SiLU transform is spread over taps
-//     NS..8, one 64-row item per tap, beside the other waves' MFMAs, instead of a block-wide
-//     transform phase between chunks;
-//   * halo rows of image segment g (HS = (rows + 2)(W + 2) each) start at g*HS; a thread
-//     stages rows of one segment only (one image's GN coefficients in registers); its rows
-//     past HS are scratch rows behind all segments.
-template <int NSEG> struct GnwCfg;
-template <> struct GnwCfg<1> { static constexpr int ITEMS = 6, NS = 4; };  // 2 x 48 KiB halo + 4 x 16 KiB ring
-template <> struct GnwCfg<4> { static constexpr int ITEMS = 7, NS = 3; };  // 2 x 56 KiB halo + 3 x 16 KiB ring
-static_assert(2 * GnwCfg<1>::ITEMS * 64 * ROWB + GnwCfg<1>::NS * TILEB <= GNW_SMEM, "LDS");
-static_assert(2 * GnwCfg<4>::ITEMS * 64 * ROWB + GnwCfg<4>::NS * TILEB <= GNW_SMEM, "LDS");
-
-template <int NSEG>
-__global__ __launch_bounds__(512, 1) void conv3x3_gn_wide_kernel(ConvArgs a) {
-  typedef bf16_t T;
-  constexpr int ITEMS = GnwCfg<NSEG>::ITEMS, NS = GnwCfg<NSEG>::NS;
-  constexpr int LPC = ITEMS + 4;                  // vector loads per lane per chunk: halo items + coefficients
-  constexpr int HALO = ITEMS * 64 * ROWB;         // one halo buffer
-  constexpr int TPS = 512 / NSEG, RPP = TPS / 8;  // threads per image segment, its halo rows per pass
-  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
-  char* wring = smem + 2 * HALO;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
-  const TileId bt = tile_of_block();
-  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
-  const int H = a.Hout, W = a.Wout, HW = H * W, W2 = W + 2;
-  const int Cin = a.C1 + a.C2, ncc = Cin / 64, nS = 9 * ncc;
-  const int THs = NSEG == 1 ? GNW_BN / W : H;  // output rows of one segment
-  const int HS = (THs + 2) * W2;
-  const int img0 = tileP / HW, y0 = (tileP - img0 * HW) / W;
-  const T* zero = zero_of_block<T>(a);
-  // measurement switch 512: static priority for the second-dispatched half (waves 4-7)
-  if ((a.dbg & 512) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-
-  int hb[2];  // halo row of this lane's B columns at tap (0,0)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pl = wn * 64 + j * 32 + rl;
-    const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-    hb[j] = seg * HS + oy * W2 + (rem - oy * W);
-  }
-  int arow[2];  // weight rows: DMA q of wave w fills rows 8*(2w+q) .. +7 of the stage
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 8 * (2 * wid + q) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int co = tileC + r;
-    arow[q] = co < a.Cout ? co * a.K + c * 8 : -1;
-  }
-  const int lch = tid & 7, sg = tid / TPS, lt = tid - sg * TPS;
-  int hrow[ITEMS], poff[ITEMS];  // LDS halo row of item j; its input pixel, or -1 (padding / scratch)
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int r = (lt >> 3) + RPP * j;
-    hrow[j] = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
-    int po = -1;
-    if (r < HS) {
-      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) po = ((img0 + sg) * H + iy) * W + ix;
-    }
-    poff[j] = po;
-  }
-  // every step issues exactly 2 weight DMAs per wave (zero page past the last stage)
-  auto issue_w = [&](int s) {
-    const int cc = s / 9, tap = s - cc * 9;
-    const int k0 = tap * Cin + cc * 64;
-    char* dst = wring + (s % NS) * TILEB;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const T* ga = (arow[q] >= 0 && s < nS && (s < NS - 1 || !(a.dbg & 1))) ? (const T*)a.wt + (unsigned)(arow[q] + k0) : zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(dst + (2 * wid + q) * 1024), 16, 0, 0);
-    }
-  };
-  f32x16 acc[2][2];
-  u32x4 hreg[ITEMS];
-  f32x4 cf[4];  // a[8], b[8] of this lane's 8 channels for its segment's image
-  // halo + coefficient loads as inline asm (outside hipcc's vmcnt bookkeeping, which would
-  // drain the weight DMAs); the counted waits of the tap loop retire them
-  auto load_chunk = [&](int cc) {
-    const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
-    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
-    const int Cs = s1 ? a.C1 : a.C2;
-    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const T* p = src + (unsigned)(poff[j] * Cs + cs0);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(hreg[j]) : "v"(poff[j] >= 0 && !(a.dbg & 64) ? p : zero) : "memory");
-    }
-    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(cf[q]) : "v"(cp + q) : "memory");
-  };
-  // item j -> silu(x*a + b) as bf16 (padding exactly 0); called only after the counted wait
-  // that retired the chunk's loads: the empty asm keeps every consumer below that point
-  auto write_item = [&](char* hbuf, int j) {
-    asm volatile("" : "+v"(hreg[j]), "+v"(cf[0]), "+v"(cf[1]), "+v"(cf[2]), "+v"(cf[3]));
-    const uint32_t* xw = (const uint32_t*)&hreg[j];
-    u32x4 y = hreg[j];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
-      if (a.dbg & 8) break;
-      const f32x2 x = {__uint_as_float(xw[w] << 16), __uint_as_float(xw[w] & 0xffff0000u)};
-      const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
-      const f32x2 sc = (w & 1) ? f32x2{av[2], av[3]} : f32x2{av[0], av[1]};
-      const f32x2 sh = (w & 1) ? f32x2{bv[2], bv[3]} : f32x2{bv[0], bv[1]};
-      const f32x2 r = gn_silu2(x, sc, sh);
-      y[w] = (uint32_t)f2bf(r.x) | ((uint32_t)f2bf(r.y) << 16);
-    }
-    const bool pad = poff[j] < 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
-    const int h = hrow[j];
-    *(u32x4*)(hbuf + h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4)) = y;
-  };
-  // The tap's 4 k-steps with the fragment reads two k-steps ahead of their MFMAs (two fragment
-  // buffers): left to itself the compiler reads each k-step right before its MFMAs and drains
-  // lgkmcnt(0) in front of every MFMA pair, exposing the LDS latency 8 times per tap.
-  auto mma_tap = [&](const char* hbuf, int s, int tap) {
-    if (a.dbg & 2) return;
-    const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
-    const char* A = wring + (s % NS) * TILEB;
-    const char* ar[2];
-    const char* br[2];
-    int bsw[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) ar[i] = A + ((a.dbg & 2048) ? 0 : (wm * 64 + i * 32 + rl) * ROWB);  // 2048: broadcast A reads
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int h = (a.dbg & 1024) ? 0 : hb[j] + toff;  // 1024: broadcast B reads (measurement only)
-      br[j] = hbuf + h * ROWB;
-      bsw[j] = (h >> 1) & 7;
-    }
-    const int asw = (rl >> 1) & 7;  // rows wm*64 + i*32 + rl: (row >> 1) & 7 == (rl >> 1) & 7
-    bf16x8 fa[2][2], fb[2][2];
-    auto rd = [&](int kk, int buf) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[buf][i] = *(const bf16x8*)(ar[i] + (((2 * kk + hh) ^ asw) << 4));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fb[buf][j] = *(const bf16x8*)(br[j] + (((2 * kk + hh) ^ bsw[j]) << 4));
-    };
-    if constexpr (NSEG == 1) {
-      rd(0, 0);
-      rd(1, 1);
-      __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the reads back to their MFMAs)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int b = kk & 1;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
-        if (kk + 2 < 4) rd(kk + 2, b);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {  // NSEG = 4 holds 7 halo items: no registers for the second fragment buffer
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        rd(kk, 0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-      }
-    }
-  };
-
-  zero_acc(acc);
-  load_chunk(0);
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue_w(s);
-  wait_vmcnt<2 * (NS - 1)>();  // the chunk-0 loads (older than the weight DMAs)
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) write_item(smem, j);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  // One chunk = 9 taps. Step s waits for its weight stage with the NS-2 younger stages (2 DMAs
-  // each) left in flight -- plus, at taps 1..NS-1, the next chunk's LPC loads issued at tap 0 --
-  // passes the barrier, refills the ring slot read at step s-1 and runs its MFMAs. The last
-  // three taps (peeled: item indices must be compile-time) also write the next chunk's halo,
-  // a third of the items each; taps 1-5 are a runtime loop (a fully unrolled chunk spills).
-  constexpr int TW = 6;
-  static_assert(TW >= NS, "the chunk's loads are retired before the first item write");
-#ifdef ITSD_STAMPS
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wait, barrier, issue, mma, transform, prologue, epilogue, total
-  const unsigned long long t_begin = stamp();
-#endif
-  auto step = [&](int s0, int tap, const char* hcur, bool lpc_in_flight) {
-    STAMP(t0);
-    if (lpc_in_flight) wait_vmcnt<2 * (NS - 2) + LPC>();
-    else wait_vmcnt<2 * (NS - 2)>();
-    STAMP(t1);
-    __builtin_amdgcn_s_barrier();
-    STAMP(t2);
-    issue_w(s0 + tap + NS - 1);
-    STAMP(t3);
-    STAMP_ADD(0, t1 - t0);
-    STAMP_ADD(1, t2 - t1);
-    STAMP_ADD(2, t3 - t2);
-  };
-  auto mma_timed = [&](const char* hbuf, int s, int tap) {
-    STAMP(m0);
-    mma_tap(hbuf, s, tap);
-    STAMP(m1);
-    STAMP_ADD(3, m1 - m0);
-  };
-  auto run_chunk = [&](int cc, auto stage) {
-    constexpr bool ST = decltype(stage)::value;
-    const int s0 = cc * 9;
-    const char* hcur = smem + (cc & 1) * HALO;
-    char* hnext = smem + ((cc + 1) & 1) * HALO;
-    step(s0, 0, hcur, false);
-    if constexpr (ST) {
-      asm volatile("" ::: "memory");
-      load_chunk(cc + 1);
-      asm volatile("" ::: "memory");
-    }
-    mma_timed(hcur, s0, 0);
-#pragma unroll 1
-    for (int tap = 1; tap < TW; ++tap) {
-      step(s0, tap, hcur, ST && tap <= NS - 1);
-      mma_timed(hcur, s0 + tap, tap);
-    }
-#pragma unroll
-    for (int k = 0; k < 9 - TW; ++k) {
-      step(s0, TW + k, hcur, false);
-      mma_timed(hcur, s0 + TW + k, TW + k);
-      if constexpr (ST) {
-        STAMP(w0);
-#pragma unroll
-        for (int j = k * ITEMS / 3; j < (k + 1) * ITEMS / 3; ++j) write_item(hnext, j);
-        STAMP(w1);
-        STAMP_ADD(4, w1 - w0);
-      }
-    }
-    if constexpr (ST) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-#ifdef ITSD_STAMPS
-  st[5] = stamp() - t_begin;  // prologue (first chunk staged)
-#endif
-  for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
-  run_chunk(ncc - 1, std::false_type{});
-  wait_vmcnt<0>();
-  __syncthreads();
-  if (a.dbg & 16) return;
-  STAMP(e0);
-  acc_to_E_wide(acc, (float*)smem);
-  __syncthreads();
-  epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
-#ifdef ITSD_STAMPS
-  __syncthreads();
-  const unsigned long long e1 = stamp();
-  st[6] = e1 - e0;
-  st[7] = e1 - t_begin;
-  if (lane == 0) {
-    const int b = (blockIdx.x + gridDim.x * blockIdx.y) & 1023;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) g_stamps[(b * 16 + wid) * 8 + q] = st[q];
-  }
-#endif
-}
-
-// ---------------------------------------------------------------------------- weights in registers
-// Fused GroupNorm+SiLU+conv3x3 with the A operand (weights) streamed straight into VGPRs.
-// The phase stamps of conv3x3_gn_wide_kernel put ~45 % of each tap outside the matrix pipe:
-// the per-tap s_barrier that retires a weight-ring slot (~430 cycles), the LDS-DMA issue of the
-// next slot (~290) and the halo transform (~250), all paid by both waves of a SIMD at the same
-// time. Here the weights never touch LDS:
-//   * weights are pre-packed in MFMA fragment order, wfrag[Cout/32][K/16][64 lanes][8 k]
-//     (bf16): one 16-B load per lane per k-step, 1 KiB per wave-instruction, fully coalesced;
-//   * wave w owns couts 32*(w&3) .. +31 (one A fragment per k-step) and pixels 128*(w>>2) .. +127
-//     (four B fragments from the LDS halo); waves w and w+4 share a SIMD and read the same
-//     weights (the second read is an L1 hit);
-//   * the A fragment of k-step s+5 is loaded while k-step s computes (a 6-slot register ring;
-//     36 k-steps per 64-channel chunk, so the slot of a k-step is static); the only block barrier
-//     is the one per chunk that publishes the next chunk's GroupNorm+SiLU'd halo
-//     (double-buffered; loaded in three item groups at taps 0/2/4 and transformed at taps 3/5/7,
-//     beside the other waves' MFMAs).
-// W (image width) is a template argument: the halo addressing divides by W + 2.
-// Per output the MFMA sequence (chunk, tap, k-step) and the epilogue are conv3x3_gn_wide_kernel's,
-// so the result is bit-identical to it.
-template <int W> struct GnrCfg;
-template <> struct GnrCfg<32> { static constexpr int NSEG = 1, ITEMS = 6; };  // 8 rows + border: 10 x 34
-template <> struct GnrCfg<16> { static constexpr int NSEG = 1, ITEMS = 6; };  // one image + border: 18 x 18
-template <> struct GnrCfg<8> { static constexpr int NSEG = 4, ITEMS = 7; };   // four images: 4 x 10 x 10
-constexpr int GNR_RING = 6;  // A k-step slots in flight (prefetch distance 5 k-steps)
-
-// AB: compile-time ablations for measurement builds only (conv_dbg 4096 + AB << 13; results wrong
-// when set): 1 no MFMA, 2 no A loads, 4 no B LDS reads, 8 no halo loads / transform, 16 no epilogue,
-// 32 no GroupNorm+SiLU arithmetic (raw halo copied), 64 no halo LDS writes.
-template <int W, int AB = 0>
-__global__ __launch_bounds__(512, 1) void conv3x3_gn_reg_kernel(ConvArgs a) {
-  typedef bf16_t T;
-  constexpr int NSEG = GnrCfg<W>::NSEG, ITEMS = GnrCfg<W>::ITEMS;
-  constexpr int W2 = W + 2;
-  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;  // output rows of one image segment (square images)
-  constexpr int HS = (THs + 2) * W2;              // halo rows of one segment
-  constexpr int HALO = ITEMS * 64 * ROWB;         // one halo buffer
-  constexpr int TPS = 512 / NSEG, RPP = TPS / 8;  // threads per image segment, its halo rows per pass
-  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  static_assert(2 * HALO <= GNW_SMEM, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar addressing
-  const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
-  const TileId bt = tile_of_block();
-  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
-  const int H = a.Hout;
-  const int Cin = a.C1 + a.C2, ncc = Cin / 64;
-  const int img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
-  const T* zero = zero_of_block<T>(a);
-
-  int hb[4];  // halo row of this lane's pixel in B tile j at tap (0,0)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int pl = wn * 128 + j * 32 + rl;
-    const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-    hb[j] = seg * HS + oy * W2 + (rem - oy * W);
-  }
-  const int kpt = Cin >> 4;  // k-steps per tap
-  // this wave's A fragments: scalar base + lane * 16 B (global_load saddr form, one VGPR offset)
-  const char* abase = (const char*)a.wfrag + (size_t)((tileC >> 5) + wm) * (9 * kpt) * 1024;
-  const int alane = lane * 16;
-  const int lch = tid & 7, sg = tid / TPS, lt = tid - sg * TPS;
-  // halo item j of this thread: row r = lt/8 + RPP*j of its segment; input pixel or -1 (padding /
-  // scratch rows past the segment, written but never read)
-  auto item_row = [&](int j) { return (lt >> 3) + RPP * j; };
-  auto item_pix = [&](int j) -> int {  // branch-free (selects, no exec-mask branches)
-    const int r = item_row(j);
-    const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-    const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    return ok ? ((img0 + sg) * H + iy) * W + ix : -1;
-  };
-  auto item_lds = [&](int j) {
-    const int r = item_row(j);
-    const int h = r < HS ? sg * HS + r : NSEG * HS + sg * (ITEMS * RPP - HS) + (r - HS);
-    return h * ROWB + ((lch ^ ((h >> 1) & 7)) << 4);
-  };
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-  u32x4 ra[GNR_RING];   // A fragments of the k-steps in flight
-  u32x4 hreg[ITEMS];    // next chunk's raw halo items (a group at a time is live)
-  f32x4 cf[4];          // a[8], b[8] of this lane's 8 channels, its segment's image, next chunk
-  auto load_a = [&](int cc, int step, u32x4& dst) {  // step = tap * 4 + kk of chunk cc
-    const int tap = step >> 2, kk = step & 3;
-    if constexpr (AB & 2) dst = u32x4{(uint32_t)step, 0u, 0u, 0u};
-    else dst = *(const u32x4*)(abase + (size_t)(tap * kpt + cc * 4 + kk) * 1024 + alane);
-  };
-  auto load_items = [&](int cc, int j0, int j1) {
-    if constexpr ((AB & 8) != 0) return;
-    const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
-    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
-    const int Cs = s1 ? a.C1 : a.C2;
-    const int cs0 = (s1 ? ci0 : ci0 - a.C1) + lch * 8;
-#pragma unroll
-    for (int j = j0; j < j1; ++j) {
-      const int po = item_pix(j);
-      hreg[j] = *(const u32x4*)(po >= 0 ? src + (unsigned)(po * Cs + cs0) : zero);
-    }
-  };
-  auto load_coef = [&](int cc) {
-    const f32x4* cp = (const f32x4*)(a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + cc * 8 + lch) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cf[q] = cp[q];
-  };
-  // silu(x*a + b) in scalar f32 (packed f32 VALU beside MFMAs costs more than it saves,
-  // MI355X_MICROARCH.md 'price of one filler'); same operations as gn_silu2, so bit-identical
-  auto gn_silu1 = [](float x, float sc, float sh) {
-    const float y = x * sc + sh;
-    return y * __builtin_amdgcn_rcpf(__expf(-y) + 1.0f);
-  };
-  auto write_item = [&](char* hbuf, int j) {
-    if constexpr ((AB & 8) != 0) return;
-    const uint32_t* xw = (const uint32_t*)&hreg[j];
-    u32x4 y = hreg[j];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {  // bf16 pair -> fp32 pair -> transform -> bf16 pair
-      if constexpr ((AB & 32) != 0) break;
-      const float x0 = __uint_as_float(xw[w] << 16), x1 = __uint_as_float(xw[w] & 0xffff0000u);
-      const f32x4 av = cf[w >> 1], bv = cf[2 + (w >> 1)];
-      const int e = 2 * (w & 1);
-      const float r0 = gn_silu1(x0, av[e], bv[e]), r1 = gn_silu1(x1, av[e + 1], bv[e + 1]);
-      y[w] = (uint32_t)f2bf(r0) | ((uint32_t)f2bf(r1) << 16);
-    }
-    const bool pad = item_pix(j) < 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = pad ? 0u : y[e];
-    if constexpr ((AB & 64) != 0) {
-      if (y[0] == 0x12345u) *(u32x4*)(hbuf + item_lds(j)) = y;
-    } else {
-      *(u32x4*)(hbuf + item_lds(j)) = y;
-    }
-  };
-  auto block_sync = [&]() {  // this wave's LDS writes done, then the workgroup barrier
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  // item groups of the next chunk's halo: loaded at taps 0 / 2 / 4, transformed at 3 / 5 / 7
-  constexpr int G1 = ITEMS / 3, G2 = 2 * (ITEMS / 3);
-
-  // Epilogue inputs staged up front. LDS map: halos [0, 2*HALO) during the loop, then the fp32
-  // tile E [256][EROW] over them; behind E: addv = bias + temb (+ CFG cond) per (image of the
-  // tile, cout) and the statistics partials of the 8 waves.
-  constexpr int NIMT = NSEG;                     // images of the tile (W = 8: four)
-  float* addv = (float*)smem + GNW_BN * EROW;    // [NIMT][128]
-  float* spart = addv + NIMT * CONV_BM;          // [8 waves][2][128]
-  static_assert((GNW_BN * EROW + NIMT * CONV_BM + 8 * 2 * CONV_BM) * 4 <= GNW_SMEM, "epilogue LDS");
-  static_assert(2 * HALO <= GNW_BN * EROW * 4, "halos lie under E");
-  {
-    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tid; it < NIMT * CONV_BM; it += 512) {
-      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
-      float v = a.bias[co];
-      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
-      if (a.cemb) {
-        int lab = 0;
-        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
-      }
-      addv[it] = v;
-    }
-  }
-  // epilogue thread map: 8 consecutive couts (ecq * 8) of 8 consecutive pixel rows (8 * erg ..),
-  // so a wave's rows (32 of them) lie in one GroupNorm statistics slot (>= 64 pixels)
-  const int ecq = tid & 15, erg = tid >> 4;
-  u32x4 rres[8];  // the residual rows, prefetched during the last chunk
-  auto load_resid = [&]() {
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      rres[k] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + 8 * erg + k) * a.Cout + tileC + ecq * 8);
-  };
-
-  // prologue: chunk 0's halo and the first 5 k-steps' weights
-  load_coef(0);
-  load_items(0, 0, ITEMS);
-#pragma unroll
-  for (int st = 0; st < GNR_RING - 1; ++st) load_a(0, st, ra[st]);
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) write_item(smem, j);
-  block_sync();
-
-  auto run_chunk = [&](int cc, auto stage) {
-    constexpr bool ST = decltype(stage)::value;
-    const char* hcur = smem + (cc & 1) * HALO;
-    char* hnext = smem + ((cc + 1) & 1) * HALO;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      if (ST && tap == 0) {
-        load_coef(cc + 1);
-        load_items(cc + 1, 0, G1);
-      }
-      if (ST && tap == 2) load_items(cc + 1, G1, G2);
-      if (ST && tap == 4) load_items(cc + 1, G2, ITEMS);
-      if (!ST && tap == 2 && a.resid) load_resid();
-      const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
-      // B addresses rebuilt per tap from an opaque copy of hb: left alone, the compiler hoists
-      // all 144 per-chunk addresses out of the chunk loop and spills them
-      int hv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        hv[j] = hb[j] + toff;
-        asm volatile("" : "+v"(hv[j]));
-      }
-      bf16x8 fb[2][4];
-      auto rd = [&](int kk, int buf) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if constexpr ((AB & 4) != 0) fb[buf][j] = bf16x8{(short)hv[j], 0, 0, 0, 0, 0, 0, (short)kk};
-          else fb[buf][j] = *(const bf16x8*)(hcur + hv[j] * ROWB + (((2 * kk + hh) ^ ((hv[j] >> 1) & 7)) << 4));
-        }
-      };
-      rd(0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int step = tap * 4 + kk;
-        // prefetch k-step step + 5 (past the chunk's end: the next chunk's first k-steps)
-        const int pf = step + GNR_RING - 1;
-        if (pf < 36) load_a(cc, pf, ra[pf % GNR_RING]);
-        else if (ST) load_a(cc + 1, pf - 36, ra[pf % GNR_RING]);
-        if (kk + 1 < 4) rd(kk + 1, (kk + 1) & 1);
-        const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if constexpr ((AB & 1) != 0) acc[j][0] += (float)af[0] + (float)fb[kk & 1][j][0];
-          else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[kk & 1][j], acc[j], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (ST && tap == 3) {
-#pragma unroll
-        for (int j = 0; j < G1; ++j) write_item(hnext, j);
-      }
-      if (ST && tap == 5) {
-#pragma unroll
-        for (int j = G1; j < G2; ++j) write_item(hnext, j);
-      }
-      if (ST && tap == 7) {
-#pragma unroll
-        for (int j = G2; j < ITEMS; ++j) write_item(hnext, j);
-      }
-    }
-    if (ST) block_sync();
-  };
-  for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
-  run_chunk(ncc - 1, std::false_type{});
-  block_sync();  // every wave is done reading the halos: the epilogue's E tile overlays them
-  float* E = (float*)smem;
-  if constexpr ((AB & 16) != 0) {  // keep the accumulators alive, skip the epilogue
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s += acc[j][r];
-    if (s == 1.2345f) E[tid] = s;
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 v4 = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
-      *(f32x4*)(E + (wn * 128 + j * 32 + rl) * EROW + wm * 32 + 8 * g + 4 * hh) = v4;
-    }
-  __syncthreads();
-  // + addv + residual, rounded once, 16-B stores; the consumer GroupNorm's per-channel (sum,
-  // sum of squares) of the rounded values accumulated in registers over the thread's 8 rows
-  const int HWo = H * W;
-  const float* av = addv + (NSEG == 1 ? 0 : (8 * erg) / HWo) * CONV_BM + ecq * 8;
-  float s8[8], q8[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s8[e] = q8[e] = 0.f;
-  const f32x4 a0 = *(const f32x4*)av, a1 = *(const f32x4*)(av + 4);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int r = 8 * erg + k;
-    const f32x4 e0 = *(const f32x4*)(E + r * EROW + ecq * 8), e1 = *(const f32x4*)(E + r * EROW + ecq * 8 + 4);
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = e0[e] + a0[e];
-      v[4 + e] = e1[e] + a1[e];
-    }
-    if (a.resid) {
-      const T* re = (const T*)&rres[k];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bf2f(re[e]);
-    }
-    u32x4 w;
-    T* we = (T*)&w;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      we[e] = f2bf(v[e]);
-      const float rv = bf2f(we[e]);
-      s8[e] += rv;
-      q8[e] = fmaf(rv, rv, q8[e]);
-    }
-    *(u32x4*)((T*)a.out + (size_t)(tileP + r) * a.Cout + tileC + ecq * 8) = w;
-  }
-  if (!a.stats) return;
-  // lanes l, l+16, l+32, l+48 hold the same 8 channels: butterfly over them, then one row of
-  // partials per wave in LDS; slot sums in fixed wave order (deterministic, no atomics)
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    s8[e] += __shfl_xor(s8[e], 16, 64);
-    q8[e] += __shfl_xor(q8[e], 16, 64);
-    s8[e] += __shfl_xor(s8[e], 32, 64);
-    q8[e] += __shfl_xor(q8[e], 32, 64);
-  }
-  if (lane < 16) {
-    float* sp = spart + (size_t)wid * 2 * CONV_BM + ecq * 8;
-    *(f32x4*)sp = f32x4{s8[0], s8[1], s8[2], s8[3]};
-    *(f32x4*)(sp + 4) = f32x4{s8[4], s8[5], s8[6], s8[7]};
-    *(f32x4*)(sp + CONV_BM) = f32x4{q8[0], q8[1], q8[2], q8[3]};
-    *(f32x4*)(sp + CONV_BM + 4) = f32x4{q8[4], q8[5], q8[6], q8[7]};
-  }
-  __syncthreads();
-  constexpr int SLOT = (NSEG == 1 ? 128 : 64);  // stat_slot_px(HW): 128, or HW = 64 at 8x8
-  constexpr int WPS = SLOT / 32;                // waves per slot
-  for (int it = tid; it < (GNW_BN / SLOT) * CONV_BM; it += 512) {
-    const int sl = it / CONV_BM, cl = it % CONV_BM;
-    float sum = 0.f, sq = 0.f;
-#pragma unroll
-    for (int w = 0; w < WPS; ++w) {
-      sum += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + cl];
-      sq += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + CONV_BM + cl];
-    }
-    const long long slot = (long long)tileP / SLOT + sl;
-    a.stats[(slot * 2) * a.Cout + tileC + cl] = sum;
-    a.stats[(slot * 2 + 1) * a.Cout + tileC + cl] = sq;
-  }
-}
-
-// ---------------------------------------------------------------------------- warp-specialized
-// conv3x3_gn_reg_kernel with the GroupNorm+SiLU halo work moved to dedicated waves. Ablations of
-// the register kernel put ~30 % of its time in the halo loads + transform (VALU that the MFMA
-// waves issued between their own MFMAs) and ~27 % in the epilogue. Here a 768-thread block runs
-//   * waves 0..7 (MFMA waves): exactly the register kernel's MFMA loop (A fragments streamed into
-//     VGPRs, B from the LDS halo, one barrier per 64-channel chunk) and nothing else;
-//   * waves 8..11 (one per SIMD, "halo waves"): load + GroupNorm+SiLU + LDS-write the next
-//     chunk's halo while the MFMA waves compute the current one (MFMA and VALU pipes run
-//     concurrently on a SIMD), prefetch the residual rows during the last chunk, and run the
-//     epilogue's output pass (+ bias/temb/residual, rounding, 16-B stores, GroupNorm statistics).
-// 3 waves per SIMD: 168 VGPRs each. The MFMA sequence per output equals the register kernel's.
+// GroupNorm+SiLU for the halo waves (conv3x3_gn_p4_kernel; diagnostic builds: also the earlier 256-pixel kernels)
 // silu(x*a + b) from coefficients prescaled by -log2(e) (a' = -a log2e, b' = -b log2e):
 // t = x a' + b' = -y log2e, 2^t = e^-y, and silu(y) = y / (1 + e^-y) = t / ((1 + 2^t)(-1/ln2))
 // -- fma, exp2, fma, rcp, mul: one VALU op fewer than fma, mul, exp2, add, rcp, mul
@@ -1713,508 +1077,6 @@ __device__ __forceinline__ void gn_silu_x4(uint32_t xa, uint32_t xb, float a0, f
       : "v"(xa), "v"(xb), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(zm),
         "s"(GN_L2E));
 }
-template <int W> struct GnsCfg;
-template <> struct GnsCfg<32> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 10 x 34 halo rows
-template <> struct GnsCfg<16> { static constexpr int NSEG = 1, ITEMS = 11; };  // 352 >= 18 x 18
-template <> struct GnsCfg<8> { static constexpr int NSEG = 4, ITEMS = 13; };   // 4 x 104 >= 4 x 10 x 10
-constexpr int GNS_MAXC = 896;  // input channels: 4 waves' GroupNorm coefficient tables fit behind the halos
-
-template <int W>
-__global__ __launch_bounds__(768, 1) void conv3x3_gn_ws_kernel(ConvArgs a) {
-  typedef bf16_t T;
-  constexpr int NSEG = GnsCfg<W>::NSEG, ITEMS = GnsCfg<W>::ITEMS;
-  constexpr int W2 = W + 2;
-  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;  // output rows of one image segment
-  constexpr int HS = (THs + 2) * W2;              // halo rows of one segment
-  constexpr int TPS = 256 / NSEG, RPP = TPS / 8;  // halo-wave threads per segment, rows per pass
-  constexpr int HROWS = NSEG * ITEMS * RPP;       // halo rows incl. scratch
-  constexpr int HALO = HROWS * ROWB;
-  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  static_assert(2 * HALO <= GNW_BN * EROW * 4, "halos lie under E");
-  __shared__ __attribute__((aligned(16))) char smem[GNW_SMEM];
-  float* const E = (float*)smem;
-  float* const addv = E + GNW_BN * EROW;        // [NSEG][128]
-  float* const spart = addv + NSEG * CONV_BM;   // [4 halo waves][2][128]
-  static_assert((GNW_BN * EROW + NSEG * CONV_BM + 4 * 2 * CONV_BM) * 4 <= GNW_SMEM, "epilogue LDS");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const TileId bt = tile_of_block();
-  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
-  const int H = a.Hout;
-  const int Cin = a.C1 + a.C2, ncc = Cin / 64;
-  const int img0 = tileP / (H * W), y0 = (tileP - img0 * H * W) / W;
-#ifdef ITSD_STAMPS
-  // MFMA waves: 0 chunk compute, 1 barrier wait, 5 prologue, 6 epilogue, 7 total; halo waves:
-  // 3 halo staging, 1 barrier wait, 5 chunk-0 staging, 6 output pass
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const unsigned long long t_begin = stamp();
-  auto stamps_out = [&]() {
-    st[7] = stamp() - t_begin;
-    if (lane == 0) {
-      const int b = (blockIdx.x + gridDim.x * blockIdx.y) & 1023;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) g_stamps[(b * 16 + wid) * 8 + q] = st[q];
-    }
-  };
-#define WS_STAMP_OUT() stamps_out()
-#else
-#define WS_STAMP_OUT()
-#endif
-  auto block_sync = [&]() {  // this wave's LDS writes done, then the workgroup barrier
-    STAMP(b0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    STAMP(b1);
-    STAMP_ADD(1, b1 - b0);
-  };
-  // addv = bias + temb (+ CFG cond) per (image of the tile, cout), behind E
-  {
-    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tid; it < NSEG * CONV_BM; it += 768) {
-      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
-      float v = a.bias[co];
-      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
-      if (a.cemb) {
-        int lab = 0;
-        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
-      }
-      addv[it] = v;
-    }
-  }
-
-  if (wid < 8) {
-    // ================================================================ MFMA waves
-    const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
-    int hb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = wn * 128 + j * 32 + rl;
-      const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
-    }
-    const int kpt = Cin >> 4;
-    const char* abase = (const char*)a.wfrag + (size_t)((tileC >> 5) + wm) * (9 * kpt) * 1024;
-    const int alane = lane * 16;
-    f32x16 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-    u32x4 ra[GNR_RING];
-    auto load_a = [&](int cc, int step, u32x4& dst) {
-      const int tap = step >> 2, kk = step & 3;
-      dst = *(const u32x4*)(abase + (size_t)(tap * kpt + cc * 4 + kk) * 1024 + alane);
-    };
-#pragma unroll
-    for (int s0 = 0; s0 < GNR_RING - 1; ++s0) load_a(0, s0, ra[s0]);
-#ifdef ITSD_STAMPS
-    st[5] = stamp() - t_begin;
-#endif
-    block_sync();  // B0: chunk 0's halo is in buffer 0
-    auto run_chunk = [&](int cc, auto stage) {
-      constexpr bool ST = decltype(stage)::value;
-      STAMP(c0);
-      const char* hcur = smem + (cc & 1) * HALO;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
-        int hv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          hv[j] = hb[j] + toff;
-          asm volatile("" : "+v"(hv[j]));
-        }
-        bf16x8 fb[2][4];
-        auto rd = [&](int kk, int buf) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            fb[buf][j] = *(const bf16x8*)(hcur + hv[j] * ROWB + (((2 * kk + hh) ^ ((hv[j] >> 1) & 7)) << 4));
-        };
-        rd(0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int step = tap * 4 + kk;
-          const int pf = step + GNR_RING - 1;
-          if (pf < 36) load_a(cc, pf, ra[pf % GNR_RING]);
-          else if (ST) load_a(cc + 1, pf - 36, ra[pf % GNR_RING]);
-          if (kk + 1 < 4) rd(kk + 1, (kk + 1) & 1);
-          const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[kk & 1][j], acc[j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      STAMP(c1);
-      STAMP_ADD(0, c1 - c0);
-      block_sync();  // chunk done (halo buffer free); next chunk's halo published
-    };
-    for (int cc = 0; cc + 1 < ncc; ++cc) run_chunk(cc, std::true_type{});
-    run_chunk(ncc - 1, std::false_type{});
-    // the last barrier above ends every halo read: E overlays the halos
-    STAMP(e0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 v4 = {acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
-        *(f32x4*)(E + (wn * 128 + j * 32 + rl) * EROW + wm * 32 + 8 * g + 4 * hh) = v4;
-      }
-    block_sync();  // E1: the fp32 tile is complete
-    if (a.stats) block_sync();  // E2 (the halo waves' statistics partials)
-#ifdef ITSD_STAMPS
-    st[6] = stamp() - e0;
-#endif
-    WS_STAMP_OUT();
-    return;
-  }
-
-  // ================================================================== halo waves
-  // Item j of this thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch).
-  // Chunk-independent per item: the input pixel (0 for padding / scratch rows: a valid address
-  // whose value is never written) and whether the row is real input (okm) or zero padding inside
-  // the halo (padm; zeroed once in both buffers, never rewritten). Scratch rows past the segment
-  // are neither written nor read.
-  const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
-  const int hw = wid - 8;  // halo wave 0..3
-  // measurement switch (conv_dbg bit 20 / 21): static priority 1 / 2 for the halo waves
-  if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);
-  if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
-  int ipix[ITEMS];
-  uint32_t okm = 0, padm = 0;
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const int r = (lt >> 3) + RPP * j;
-    const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-    const bool in = iy >= 0 && iy < H && ix >= 0 && ix < W;
-    const bool ok = r < HS && in;
-    ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
-    okm |= (uint32_t)ok << j;
-    padm |= (uint32_t)(r < HS && !in) << j;
-  }
-  // LDS byte offset of item j in buffer 0: row h = sg*HS + r, 16-B chunk lch swizzled by (h>>1)&7;
-  // with RPP a multiple of 16 the swizzle is the same for every item, with RPP = 8 it alternates
-  const int hrow0 = sg * HS + (lt >> 3), hrow1 = hrow0 + RPP;
-  const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
-  const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
-  auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
-  static_assert(HROWS > NSEG * HS, "a scratch row exists");
-  const int dump = NSEG * HS * ROWB + (lch << 4);  // never read
-  // GroupNorm coefficient table of this wave's image (every chunk: 8 lanes' a[8], b[8]), private to
-  // the wave (its own writes, no barrier), in the E area behind the halos until the epilogue
-  float* const ctab = (float*)(smem + 2 * HALO) + hw * (GNS_MAXC / 8) * 16;
-  static_assert(2 * HALO + 4 * (GNS_MAXC / 8) * 64 <= GNW_BN * EROW * 4, "coefficient tables lie under E");
-  {
-    constexpr int NP = (GNS_MAXC / 8) * 4 / 64;  // 16-B pieces per lane at most
-    const int nent = ncc * 8 * 4;
-    const f32x4* src = (const f32x4*)(a.gn_coef + (size_t)(img0 + (NSEG == 1 ? 0 : hw)) * (Cin / 8) * 16);
-    f32x4 tp[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k)
-      if (lane + 64 * k < nent) tp[k] = src[lane + 64 * k];
-#pragma unroll
-    for (int k = 0; k < NP; ++k)
-      if (lane + 64 * k < nent) *(f32x4*)(ctab + (lane + 64 * k) * 4) = tp[k] * GN_L2E;  // prescaled: gn_silu_l2
-  }
-  // Chunk cc's item j: a buffer load (32-bit byte offset into its source -- src1, or src2, the
-  // concatenated skip input -- the chunk's channel offset in soffset; past the last chunk a
-  // zero-record descriptor: the load returns 0 and touches no memory, so every reload is
-  // unconditional). Item j's register is reloaded with the next chunk's item j right after its
-  // transform: ITEMS loads stay in flight, each for about one MFMA chunk before its use.
-  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
-  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
-  struct ChunkSrc {
-    __amdgpu_buffer_rsrc_t rs;
-    uint32_t rowb, so;
-  };
-  auto chunk_src = [&](int cc) __attribute__((always_inline)) {  // scalar selects only (uniform)
-    const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
-    ChunkSrc c;
-    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0,
-                                             s1 ? nrec1 : (ci0 < Cin ? nrec2 : 0), 0x00020000);
-    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
-    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
-    return c;
-  };
-  u32x4 h[ITEMS];
-  auto load_item = [&](const ChunkSrc& c, int j) __attribute__((always_inline)) {
-    h[j] = __builtin_amdgcn_raw_buffer_load_b128(c.rs, __umul24((uint32_t)ipix[j], c.rowb) + lch * 16, c.so, 0);
-  };
-  // silu(x*a + b) per channel pair (same operations as gn_silu2: fma, exp2(-log2e*y), +1, rcp,
-  // mul), rounded to a bf16 pair; written to the LDS halo where the row is real input
-  typedef __attribute__((ext_vector_type(2))) float f32x2;
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-  auto emit = [&](int cc, char* hbuf) __attribute__((always_inline)) {
-    f32x4 c[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = *(const f32x4*)(ctab + (cc * 8 + lch) * 16 + q * 4);
-    const ChunkSrc nx = chunk_src(cc + 1);
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      u32x4 y;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        // scalar f32 (packed f32 VALU beside MFMAs costs ~22 cycles an instruction,
-        // MI355X_MICROARCH.md 'price of one filler'; the file is built without SLP packing)
-        const uint32_t xw = h[j][w];
-        const int e = 2 * (w & 1);
-        const float s0 = gn_silu_l2(__uint_as_float(xw << 16), c[w >> 1][e], c[2 + (w >> 1)][e]);
-        const float s1 = gn_silu_l2(__uint_as_float(xw & 0xffff0000u), c[w >> 1][e + 1], c[2 + (w >> 1)][e + 1]);
-        y[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{s0, s1}, bf16x2_t));
-      }
-      // the reload strictly after the transform (same basic block: the store below is not
-      // conditional -- rows that are not real input go to a scratch row -- so the transform is
-      // not sunk under a branch behind the reload, which costs a second register set + copies)
-      *(u32x4*)(hbuf + (((okm >> j) & 1) ? item_lds(j) : dump)) = y;
-      __builtin_amdgcn_sched_barrier(0);
-      load_item(nx, j);
-    }
-  };
-  {
-    const ChunkSrc c0 = chunk_src(0);
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) load_item(c0, j);
-  }
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j)
-    if ((padm >> j) & 1) {
-      *(u32x4*)(smem + item_lds(j)) = u32x4{0u, 0u, 0u, 0u};
-      *(u32x4*)(smem + HALO + item_lds(j)) = u32x4{0u, 0u, 0u, 0u};
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's coefficient table is written
-  emit(0, smem);
-#ifdef ITSD_STAMPS
-  st[5] = stamp() - t_begin;
-#endif
-  block_sync();  // B0
-  for (int cc = 0; cc + 1 < ncc; ++cc) {
-    STAMP(h0);
-    emit(cc + 1, smem + ((cc + 1) & 1) * HALO);  // while the MFMA waves compute chunk cc
-#ifdef ITSD_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-    STAMP(h1);
-    STAMP_ADD(3, h1 - h0);
-    block_sync();  // end of MFMA chunk cc
-  }
-  // last chunk: prefetch the residual rows of this thread's epilogue share
-  const int ecq = tt & 15, erg = tt >> 4;  // 8 couts (ecq*8) of 16 rows (16*erg ..)
-  u32x4 rres[16];
-  if (a.resid) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      rres[k] = *(const u32x4*)((const T*)a.resid + (size_t)(tileP + 16 * erg + k) * a.Cout + tileC + ecq * 8);
-  }
-  block_sync();  // end of the last MFMA chunk
-  block_sync();  // E1
-  STAMP(o0);
-  // output pass: + addv + residual, rounded once, 16-B stores, the consumer GroupNorm's
-  // per-channel (sum, sum of squares) of the rounded values
-  const int HWo = H * W;
-  const float* av = addv + (NSEG == 1 ? 0 : (16 * erg) / HWo) * CONV_BM + ecq * 8;
-  const f32x4 a0 = *(const f32x4*)av, a1 = *(const f32x4*)(av + 4);
-  float s8[8], q8[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s8[e] = q8[e] = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int r = 16 * erg + k;
-    const f32x4 e0 = *(const f32x4*)(E + r * EROW + ecq * 8), e1 = *(const f32x4*)(E + r * EROW + ecq * 8 + 4);
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = e0[e] + a0[e];
-      v[4 + e] = e1[e] + a1[e];
-    }
-    if (a.resid) {
-      const T* re = (const T*)&rres[k];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bf2f(re[e]);
-    }
-    u32x4 w;
-    T* we = (T*)&w;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      we[e] = f2bf(v[e]);
-      const float rv = bf2f(we[e]);
-      s8[e] += rv;
-      q8[e] = fmaf(rv, rv, q8[e]);
-    }
-    *(u32x4*)((T*)a.out + (size_t)(tileP + r) * a.Cout + tileC + ecq * 8) = w;
-  }
-  if (!a.stats) {
-#ifdef ITSD_STAMPS
-    st[6] = stamp() - o0;
-#endif
-    WS_STAMP_OUT();
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    s8[e] += __shfl_xor(s8[e], 16, 64);
-    q8[e] += __shfl_xor(q8[e], 16, 64);
-    s8[e] += __shfl_xor(s8[e], 32, 64);
-    q8[e] += __shfl_xor(q8[e], 32, 64);
-  }
-  // halo wave hw: rows 64*hw .. +63
-  if (lane < 16) {
-    float* sp = spart + (size_t)hw * 2 * CONV_BM + ecq * 8;
-    *(f32x4*)sp = f32x4{s8[0], s8[1], s8[2], s8[3]};
-    *(f32x4*)(sp + 4) = f32x4{s8[4], s8[5], s8[6], s8[7]};
-    *(f32x4*)(sp + CONV_BM) = f32x4{q8[0], q8[1], q8[2], q8[3]};
-    *(f32x4*)(sp + CONV_BM + 4) = f32x4{q8[4], q8[5], q8[6], q8[7]};
-  }
-  block_sync();  // E2
-  constexpr int SLOT = (NSEG == 1 ? 128 : 64);  // stat_slot_px(HW)
-  constexpr int WPS = SLOT / 64;                // halo waves per slot
-  for (int it = tt; it < (GNW_BN / SLOT) * CONV_BM; it += 256) {
-    const int sl = it / CONV_BM, cl = it % CONV_BM;
-    float sum = 0.f, sq = 0.f;
-#pragma unroll
-    for (int w = 0; w < WPS; ++w) {
-      sum += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + cl];
-      sq += spart[(size_t)(sl * WPS + w) * 2 * CONV_BM + CONV_BM + cl];
-    }
-    const long long slot = (long long)tileP / SLOT + sl;
-    a.stats[(slot * 2) * a.Cout + tileC + cl] = sum;
-    a.stats[(slot * 2 + 1) * a.Cout + tileC + cl] = sq;
-  }
-#ifdef ITSD_STAMPS
-  st[6] = stamp() - o0;
-#endif
-  WS_STAMP_OUT();
-}
-
-// Plain implicit-GEMM conv (conv_pipe's work: 3x3 stride 2, the 4x4 level's 3x3s, 1x1s) at
-// 256 pixels: each 48 KiB stage (16 KiB of weights + 32 KiB of gathered pixel rows, both by
-// global_load_lds) through a 3-deep ring, 2 stages in flight. Under-filled grids split K over
-// gridDim.z: slices store fp32 partial tiles and splitk_wide_epilogue_kernel sums them in
-// slice order (deterministic).
-constexpr int CPW_NS = 3, CPW_STAGE = 3 * TILEB;
-constexpr int CPW_SMEM = CPW_NS * CPW_STAGE > GNW_EPI ? CPW_NS * CPW_STAGE : GNW_EPI;
-static_assert(CPW_SMEM <= GNW_SMEM, "LDS");
-
-__global__ __launch_bounds__(512, 1) void conv_pipe_wide(ConvArgs a) {
-  typedef bf16_t T;
-  constexpr int NS = CPW_NS, BK = 64;
-  __shared__ __attribute__((aligned(16))) char smem[CPW_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
-  const TileId bt = tile_of_block();
-  const int tileP = bt.x * GNW_BN, tileC = bt.y * CONV_BM;
-  const int Cin = a.C1 + a.C2, cpt = Cin / BK, nK = a.ksize * a.ksize * cpt;
-  const int HWo = a.Hout * a.Wout;
-  const T* zero = zero_of_block<T>(a);
-  // DMA rows: weights, instruction q of wave w -> rows 8*(2w+q) ..; pixels -> rows 8*(4w+q) ..
-  const T* arow[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 8 * (2 * wid + q) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int co = tileC + r;
-    arow[q] = co < a.Cout ? (const T*)a.wt + (size_t)co * a.K + c * 8 : nullptr;
-  }
-  int pix1[4], pix2[4];
-  unsigned tmask[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = 8 * (4 * wid + q) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int p = tileP + r;
-    const bool pv = p < a.M;
-    const int img = p / HWo, rem = p - img * HWo, oy = rem / a.Wout;
-    const int iy0 = oy * a.stride - a.pad, ix0 = (rem - oy * a.Wout) * a.stride - a.pad;
-    const int pl = (img * a.Hin + iy0) * a.Win + ix0;
-    pix1[q] = pl * a.C1 + c * 8;
-    pix2[q] = pl * a.C2 + c * 8;
-    unsigned m = 0;
-    for (int ky = 0; ky < a.ksize; ++ky)
-      for (int kx = 0; kx < a.ksize; ++kx) {
-        const int iy = iy0 + ky, ix = ix0 + kx;
-        if (pv && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win) m |= 1u << (ky * a.ksize + kx);
-      }
-    tmask[q] = m;
-  }
-  auto issue = [&](int kc) {
-    const int tap = kc / cpt, ci0 = (kc - tap * cpt) * BK;
-    const int ky = tap / a.ksize, kx = tap - ky * a.ksize;
-    char* sA = smem + (kc % NS) * CPW_STAGE;
-    char* sB = sA + TILEB;
-    const bool s1 = ci0 < a.C1;
-    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
-    const int toff = (ky * a.Win + kx) * (s1 ? a.C1 : a.C2) + (s1 ? ci0 : ci0 - a.C1);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const T* ga = arow[q] ? arow[q] + (size_t)kc * BK : zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, (lds_ptr_t)(sA + (2 * wid + q) * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const T* gb = ((tmask[q] >> tap) & 1u) ? src + (s1 ? pix1[q] : pix2[q]) + toff : zero;
-      __builtin_amdgcn_global_load_lds((const void*)gb, (lds_ptr_t)(sB + (4 * wid + q) * 1024), 16, 0, 0);
-    }
-  };
-  f32x16 acc[2][2];
-  zero_acc(acc);
-  const int S = gridDim.z, z = bt.z;
-  const int k0 = (int)((long long)nK * z / S), k1 = (int)((long long)nK * (z + 1) / S);
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (k0 + s < k1) issue(k0 + s);
-  for (int kc = k0; kc < k1; ++kc) {
-    if (kc + 1 < k1) wait_vmcnt<6>();  // the one younger stage (6 DMAs per wave) stays in flight
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kc + NS - 1 < k1) issue(kc + NS - 1);
-    const char* A = smem + (kc % NS) * CPW_STAGE;
-    mma_stage<T>(A, A + TILEB, acc, wm, wn, rl, hh);
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  if (S > 1) {  // partial tile: slab[tile][slice][thread][64]
-    float* mine = a.splitk_ws + (((size_t)bt.y * gridDim.x + bt.x) * S + z) * 32768 + tid * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          *(f32x4*)(mine + (i * 2 + j) * 16 + 4 * g) = v;
-        }
-    return;
-  }
-  acc_to_E_wide(acc, (float*)smem);
-  __syncthreads();
-  epilogue_from_E<T, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
-}
-
-__global__ __launch_bounds__(512, 1) void splitk_wide_epilogue_kernel(ConvArgs a, int S) {
-  __shared__ __attribute__((aligned(16))) char smem[GNW_EPI];
-  const int tileP = blockIdx.x * GNW_BN, tileC = blockIdx.y * CONV_BM;
-  const float* src = a.splitk_ws + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * S * 32768 + threadIdx.x * 64;
-  f32x16 acc[2][2];
-  zero_acc(acc);
-  for (int z = 0; z < S; ++z, src += 32768) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = *(const f32x4*)(src + (i * 2 + j) * 16 + 4 * g);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
-        }
-  }
-  acc_to_E_wide(acc, (float*)smem);
-  __syncthreads();
-  epilogue_from_E<bf16_t, CONV_BM, GNW_BN, 512>(a, smem, tileP, tileC, -1);
-}
 
 // ---------------------------------------------------------------------------- persistent, warp-specialized
 // conv3x3_gn_ws_kernel's stamps (profiles/r02_ws_stamps.txt): the MFMA waves keep the matrix pipe
@@ -2242,467 +1104,12 @@ template <> struct GnpCfg<32> { static constexpr int NSEG = 1, ITEMS = 11, RES =
 template <> struct GnpCfg<16> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 0; };  // LDS: residual from HBM
 
-// AB: compile-time ablations for measurement builds only (conv_dbg 4096 + AB << 13 with gn_reg=3,
-// W = 32; results wrong when set): 1 no MFMA (a VALU add keeps the accumulators live), 2 no
-// GroupNorm+SiLU transform in the halo waves (raw copy), 4 no register epilogue, 8 no A-fragment
-// loads (constant weights), 16 no B-fragment LDS reads.
-template <int W, int AB = 0>
-__global__ __launch_bounds__(768, 1) void conv3x3_gn_pws_kernel(ConvArgs a) {
-  typedef bf16_t T;
-  constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = GnpCfg<W>::ITEMS, RES = GnpCfg<W>::RES;
-  constexpr int W2 = W + 2;
-  constexpr int THs = NSEG == 1 ? GNW_BN / W : W;
-  constexpr int HS = (THs + 2) * W2;
-  constexpr int TPS = 256 / NSEG, RPP = TPS / 8;
-  constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
-  constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
-  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4];
-  char* const rlds = smem + 2 * HALO;
-  float* const addv = (float*)(smem + 2 * HALO + RESB);  // [2 tile parities][NSEG][128]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.Hout;
-  const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
-  const int nTC = a.Cout / CONV_BM, NT = (a.M / GNW_BN) * nTC;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int ntiles = b < NT ? (NT - 1 - b) / G + 1 : 0;
-  const int nstages = ntiles * ncc;
-  auto tile_p = [&](int k) { return ((b + k * G) / nTC) * GNW_BN; };
-  auto tile_c = [&](int k) { return ((b + k * G) % nTC) * CONV_BM; };
-#ifdef ITSD_STAMPS
-  // MFMA waves: 0 chunk compute, 1 barrier wait, 6 epilogues, 7 total; halo waves: 3 stage
-  // transforms (incl. next-stage load issue), 1 barrier wait, 5 prologue (stage 0), 7 total
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const unsigned long long t_begin = stamp();
-  auto stamps_out = [&]() {
-    st[7] = stamp() - t_begin;
-    if (lane == 0) {
-      const int bb = blockIdx.x & 1023;
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) g_stamps[(bb * 16 + wid) * 8 + qq] = st[qq];
-    }
-  };
-#define PWS_STAMP_OUT() stamps_out()
-#else
-#define PWS_STAMP_OUT()
+#ifdef ITSD_DIAG
+// Diagnostic builds only (hipcc -DITSD_DIAG, tools/build_diag.sh): the superseded 256-pixel fused-conv
+// generations (LDS weight ring, weights in registers, warp-specialised, two MFMA waves per SIMD) and the
+// 256-pixel plain conv, kept as A/B references for measurements. Never in the shipped library.
+#include "conv_diag.inc"
 #endif
-  auto block_sync = [&]() {
-    STAMP(b0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    STAMP(b1);
-    STAMP_ADD(1, b1 - b0);
-  };
-  if (ntiles == 0) return;  // (the host launches gridDim.x <= tiles)
-
-  if (wid < 8) {
-    // ================================================================ MFMA waves
-    const int wm = wid & 3, wn = wid >> 2, rl = lane & 31, hh = lane >> 5;
-    int hb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = wn * 128 + j * 32 + rl;
-      const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
-    }
-    auto abase_of = [&](int k) {
-      return (const char*)a.wfrag + (size_t)((tile_c(k) >> 5) + wm) * (9 * kpt) * 1024 + lane * 16;
-    };
-    f32x16 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-    u32x4 ra[GNR_RING];
-    {
-      const char* ab0 = abase_of(0);
-#pragma unroll
-      for (int s0 = 0; s0 < GNR_RING - 1; ++s0)
-        ra[s0] = *(const u32x4*)(ab0 + (size_t)((s0 >> 2) * kpt + (s0 & 3)) * 1024);
-    }
-    block_sync();  // B0: stage 0 staged
-    int q = 0;     // stage (chunk) counter of this block
-    for (int k = 0; k < ntiles; ++k) {
-      const int tileP = tile_p(k), tileC = tile_c(k);
-      const char* ab = abase_of(k);
-      const char* abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
-      for (int cc = 0; cc < ncc; ++cc, ++q) {
-        const char* hcur = smem + (q & 1) * HALO;
-        // the next stage's A stream: this tile's next chunk, the next tile's first chunk, or
-        // (last stage) a harmless re-read of this chunk
-        const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 4 * 1024 : (k + 1 < ntiles ? abn : ab);
-        const char* cb = ab + (size_t)cc * 4 * 1024;
-        STAMP(c0);
-        // 36 k-steps (9 taps x 4): B fragments one k-step ahead, across tap boundaries; B fragment
-        // j of tap t sits at row h = hb[j] + toff(t), 16-B chunk (2kk + hh) ^ ((h >> 1) & 7), i.e.
-        // byte offset (h * 128 + ((hh ^ sw) << 4)) ^ (kk << 5) -- one XOR per read (the halo
-        // buffers are 128-B aligned, so the XOR only touches the chunk bits)
-        int bo[4];
-        auto tap_offsets = [&](int tap) {
-          const int ky = tap / 3, kx = tap - ky * 3, toff = ky * W2 + kx;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int h = hb[j] + toff;
-            asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
-            bo[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
-          }
-        };
-        bf16x8 fb[2][4];
-        auto rd = [&](int kk, int buf) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if constexpr ((AB & 16) != 0) fb[buf][j] = bf16x8{(short)bo[j], 0, 0, 0, 0, 0, 0, (short)kk};
-            else fb[buf][j] = *(const bf16x8*)(smem + (bo[j] ^ (kk << 5)));
-          }
-        };
-        tap_offsets(0);
-        rd(0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int step = 0; step < 36; ++step) {
-          const int kk = step & 3;
-          const int pf = step + GNR_RING - 1;
-          if constexpr ((AB & 8) != 0) ra[pf % GNR_RING] = u32x4{(uint32_t)pf, (uint32_t)q, 0u, 0u};
-          else if (pf < 36) ra[pf % GNR_RING] = *(const u32x4*)(cb + (size_t)((pf >> 2) * kpt + (pf & 3)) * 1024);
-          else ra[pf % GNR_RING] = *(const u32x4*)(nb + (size_t)(((pf - 36) >> 2) * kpt + ((pf - 36) & 3)) * 1024);
-          if (step + 1 < 36) {
-            if (kk == 3) tap_offsets((step + 1) >> 2);
-            rd((step + 1) & 3, (step + 1) & 1);
-          }
-          const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % GNR_RING]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if constexpr ((AB & 1) != 0) acc[j][0] += __builtin_bit_cast(float, (uint32_t)fb[step & 1][j][0] << 16) + (float)af[0];
-            else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step & 1][j], acc[j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        STAMP(c1);
-        STAMP_ADD(0, c1 - c0);
-        block_sync();  // end of stage q: its buffer is free, stage q+1 is published
-      }
-      STAMP(e0);
-      if constexpr ((AB & 4) == 0) {
-      // ---- epilogue of tile k from the accumulators (no LDS tile, no barrier)
-      // lane (rl, hh): pixels p_j = wn*128 + 32j + rl, couts c = wm*32 + 8g + 4hh + i
-      const float* av = addv + (k & 1) * NSEG * CONV_BM + wm * 32 + 4 * hh;
-      const bool has_res = a.resid != nullptr;
-      float s16[16], q16[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int p = wn * 128 + j * 32 + rl;
-        const float* avj = av + (NSEG == 1 ? 0 : (wn * 2 + (j >> 1))) * CONV_BM;
-        uint32_t wv[4][2];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = wm * 32 + 8 * g + 4 * hh;
-          const f32x4 ad = *(const f32x4*)(avj + 8 * g);
-          uint2 rr;
-          if constexpr (RES) {
-            rr = *(const uint2*)(rlds + p * 256 + ((((c >> 3) ^ (p & 15)) << 4) | ((c & 4) << 1)));
-          } else {
-            const T* rp = has_res ? (const T*)a.resid + (size_t)(tileP + p) * a.Cout + tileC + c
-                                  : (const T*)zero_of_block<T>(a);
-            rr = *(const uint2*)rp;
-          }
-          if (!has_res) rr = uint2{0u, 0u};  // select, not a branch
-          float v[4];
-          v[0] = acc[j][4 * g + 0] + ad[0] + __uint_as_float(rr.x << 16);
-          v[1] = acc[j][4 * g + 1] + ad[1] + __uint_as_float(rr.x & 0xffff0000u);
-          v[2] = acc[j][4 * g + 2] + ad[2] + __uint_as_float(rr.y << 16);
-          v[3] = acc[j][4 * g + 3] + ad[3] + __uint_as_float(rr.y & 0xffff0000u);
-          const T b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
-          wv[g][0] = (uint32_t)b0 | ((uint32_t)b1 << 16);
-          wv[g][1] = (uint32_t)b2 | ((uint32_t)b3 << 16);
-          const float r0 = bf2f(b0), r1 = bf2f(b1), r2 = bf2f(b2), r3 = bf2f(b3);
-          s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
-          s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
-          s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
-          s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
-        }
-        // 16-B stores: v_permlane32_swap hands lane (rl, 0) its partner's upper couts of g0 and lane
-        // (rl, 1) its partner's lower couts of g1 -- each lane then owns 8 consecutive couts
-#pragma unroll
-        for (int gp = 0; gp < 4; gp += 2) {
-          u32x4 o;
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
-            o[d] = sw[0];      // hh 0: own g0 lower;  hh 1: partner's g1 lower
-            o[2 + d] = sw[1];  // hh 0: partner's g0 upper;  hh 1: own g1 upper
-          }
-          const int c8 = wm * 32 + 8 * (gp + hh);
-          *(u32x4*)((T*)a.out + (size_t)(tileP + p) * a.Cout + tileC + c8) = o;
-        }
-        // statistics slot complete: W = 8 after every image (2 pixel tiles), else after all 4
-        if (a.stats && ((NSEG == 1 && j == 3) || (NSEG != 1 && (j & 1)))) {
-          // sums over the 32 pixel lanes of each half by recursive halving: at the step of
-          // width w (16, 8, 4, 2, 1) a lane keeps the upper or lower w of its values by bit w of
-          // rl and adds its xor-w partner's copy of them -- 31 exchanges instead of 5 x 32. Lane rl
-          // ends with value rl: s16[rl] (rl < 16) or q16[rl - 16]. Exchanges: DPP quad_perm (1, 2),
-          // row_ror:8 (8), ds_swizzle xor (4, 16).
-          float v[32];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            v[e] = s16[e];
-            v[16 + e] = q16[e];
-          }
-          auto xchg = [](float x, auto wc) {
-            constexpr int w = decltype(wc)::value;
-            const int xi = __builtin_bit_cast(int, x);
-            int r;
-            if constexpr (w == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
-            else if constexpr (w == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
-            else if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
-            else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (w << 10));
-            return __builtin_bit_cast(float, r);
-          };
-          auto halve = [&](auto wc) {
-            constexpr int w = decltype(wc)::value;
-            const bool up = (rl & w) != 0;
-#pragma unroll
-            for (int i = 0; i < w; ++i) {
-              const float lo = v[i], hi = v[i + w];
-              v[i] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
-            }
-          };
-          halve(std::integral_constant<int, 16>{});
-          halve(std::integral_constant<int, 8>{});
-          halve(std::integral_constant<int, 4>{});
-          halve(std::integral_constant<int, 2>{});
-          halve(std::integral_constant<int, 1>{});
-          {
-            constexpr int SLOT = NSEG == 1 ? 128 : 64;
-            const long long slot = (long long)(tileP + wn * 128 + (NSEG == 1 ? 0 : (j >> 1) * 64)) / SLOT;
-            const int e = rl & 15, co = wm * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
-            a.stats[(slot * 2 + (rl >> 4)) * a.Cout + tileC + co] = v[0];
-          }
-#pragma unroll
-          for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
-        }
-      }
-      } else {  // keep the accumulators alive
-        float sm = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sm += acc[j][r];
-        if (sm == 1.2345f) ((float*)a.out)[0] = sm;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-      STAMP(e1);
-      STAMP_ADD(6, e1 - e0);
-    }
-    PWS_STAMP_OUT();
-    return;
-  }
-
-  // ================================================================== halo waves
-  // (conv3x3_gn_ws_kernel's halo pipeline, over the block's whole stage sequence.) Item j of this
-  // thread = halo row (lt >> 3) + RPP * j of its image segment, 8 channels (lch). Per tile, for
-  // the loads: the input pixel of each item (0 for padding / scratch rows: a valid address,
-  // never used); for the LDS writes: each item's address (its halo row, or a dump row past the
-  // segments for scratch rows) and a mask that zeroes padding rows (rewritten every stage: the
-  // padding rows differ between tiles). Stage and tile indices advance by counters (no divides).
-  const int tt = tid - 512, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
-  static_assert(NSEG * ITEMS * RPP > NSEG * HS, "a scratch row exists");
-  if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);  // measurement switches, as in the ws kernel
-  if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
-  const int dump = NSEG * HS * ROWB + (lch << 4);
-  const int hrow0 = sg * HS + (lt >> 3), hrow1 = hrow0 + RPP;
-  const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
-  const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
-  auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
-  auto tile_y0img = [&](int k, int& img0, int& y0) {
-    const int tileP = tile_p(k);
-    img0 = tileP / (H * W);
-    y0 = (tileP - img0 * H * W) / W;
-  };
-  int ipix[ITEMS];
-  const float* cbase;  // GroupNorm coefficients of the loading tile's image, this lane's 8 channels
-  auto geometry_pix = [&](int k) __attribute__((always_inline)) {
-    int img0, y0;
-    tile_y0img(k, img0, y0);
-    // the item geometry from an opaque copy of lt: hoisted out of the stage loop (it is tile-
-    // invariant), it would hold ~30 registers for good and starve the transform of temporaries
-    int ltv = lt;
-    asm volatile("" : "+v"(ltv));
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const int r = (ltv >> 3) + RPP * j;
-      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-      const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
-    }
-    cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
-  };
-  // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
-  // address is chosen once; the other items' addresses are lds0/lds1 plus constants.
-  static_assert(ITEMS * RPP - HS < RPP, "scratch rows only in the last item");
-  const int waddr_last = ((lt >> 3) + RPP * (ITEMS - 1)) < HS ? item_lds(ITEMS - 1) : dump;
-  auto waddr = [&](int j) { return j == ITEMS - 1 ? waddr_last : item_lds(j); };
-  int inm = 0;  // bit j: item j's row is real input (or scratch) -- else zero padding
-  auto geometry_emit = [&](int k) __attribute__((always_inline)) {
-    int img0, y0;
-    tile_y0img(k, img0, y0);
-    int ltv = lt;
-    asm volatile("" : "+v"(ltv));
-    inm = 0;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const int r = (ltv >> 3) + RPP * j;
-      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-      const bool in = r >= HS || (iy >= 0 && iy < H && ix >= 0 && ix < W);
-      inm |= (int)in << j;
-    }
-  };
-  // stage loads: buffer loads (32-bit byte offset into src1, or src2 = the concatenated skip
-  // input; the chunk's channel offset in soffset); past the last stage a zero-record descriptor,
-  // so every reload is unconditional (a conditional one keeps the old value alive beside the new
-  // one: a second register set the compiler rotates with waiting copies)
-  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
-  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
-  struct Src {
-    __amdgpu_buffer_rsrc_t rs;
-    uint32_t rowb, so;
-  };
-  auto src_of = [&](int cc, bool live) __attribute__((always_inline)) {  // scalar selects only (uniform)
-    const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
-    Src c;
-    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0,
-                                             live ? (s1 ? nrec1 : nrec2) : 0, 0x00020000);
-    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
-    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
-    return c;
-  };
-  auto stage_addv = [&](int k) {
-    const int tileP = tile_p(k), tileC = tile_c(k), img0 = tileP / (H * W);
-    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tt; it < NSEG * CONV_BM; it += 256) {
-      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
-      float v = a.bias[co];
-      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
-      if (a.cemb) {
-        int lab = 0;
-        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
-      }
-      addv[(k & 1) * NSEG * CONV_BM + it] = v;
-    }
-  };
-  // residual rows of tile k -> LDS by LDS-DMA (16 B a lane, 1 KiB a wave-instruction, no
-  // registers): row p, 16-B unit u of its 256 B lands at unit u ^ (p & 15) (source-side inverse
-  // swizzle), which the MFMA waves' 8-B reads in the accumulator layout hit conflict-free
-  auto res_dma = [&](int k) __attribute__((always_inline)) {
-    if constexpr (RES) {
-      const int tileP = tile_p(k), tileC = tile_c(k), hw = wid - 8;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {  // wave hw: rows 64*hw + 4*i .. +3, lane -> (row, slot)
-        const int row = 64 * hw + 4 * i + (lane >> 4), slot = lane & 15, u = slot ^ (row & 15);
-        const T* src = (const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + u * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(rlds + (64 * hw + 4 * i) * 256), 16, 0, 0);
-      }
-    }
-  };
-  u32x4 h[ITEMS];
-  f32x4 c[4], cn[4];
-  auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) c[q][e] = cn[q][e] * GN_L2E;
-  };
-  // the stage being loaded: tile kL, chunk ccL (the emitted stage is the one before it)
-  int kL = 0, ccL = 0;
-  // transform the emitted stage (items in h, coefficients in c) into hbuf; each item's register
-  // is reloaded with the loaded stage's item right after its transform; that stage's
-  // coefficients go to cn first (older than every item reload: waiting for them never waits for
-  // an item).
-  auto emit = [&](char* hbuf) __attribute__((always_inline)) {
-    if (ccL == 0) geometry_emit(kL);  // the emitted stage opens tile kL
-    if (++ccL == ncc) {
-      ccL = 0;
-      if (++kL < ntiles) geometry_pix(kL);
-    }
-    const bool live = kL < ntiles;
-    const f32x4* cp = (const f32x4*)(cbase + (live ? ccL : 0) * 128);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cn[q] = cp[q];
-    const Src nx = src_of(ccL, live);
-    typedef __attribute__((ext_vector_type(2))) float f32x2;
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const uint32_t zm = (uint32_t)__builtin_amdgcn_sbfe(inm, j, 1);  // 0 (padding) or ~0
-      uint32_t yw[4];
-      if constexpr ((AB & 2) != 0) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) yw[w] = h[j][w] & zm;
-      } else
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)  // channels 4hf .. 4hf+3: words 2hf, 2hf+1
-        gn_silu_x4(h[j][2 * hf], h[j][2 * hf + 1], c[hf][0], c[hf][1], c[hf][2], c[hf][3], c[2 + hf][0],
-                   c[2 + hf][1], c[2 + hf][2], c[2 + hf][3], zm, yw[2 * hf], yw[2 * hf + 1]);
-      const u32x4 y = {yw[0], yw[1], yw[2], yw[3]};
-      *(u32x4*)(hbuf + waddr(j)) = y;
-      __builtin_amdgcn_sched_barrier(0);
-      h[j] = __builtin_amdgcn_raw_buffer_load_b128(nx.rs, __umul24((uint32_t)ipix[j], nx.rowb) + lch * 16, nx.so, 0);
-    }
-    prescale();
-  };
-  // prologue: stage 0 (and tile 0's addv)
-  geometry_pix(0);
-  {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cn[q] = ((const f32x4*)cbase)[q];
-    prescale();
-    const Src s0 = src_of(0, true);
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j)
-      h[j] = __builtin_amdgcn_raw_buffer_load_b128(s0.rs, __umul24((uint32_t)ipix[j], s0.rowb) + lch * 16, s0.so, 0);
-  }
-  stage_addv(0);
-  emit(smem);
-#ifdef ITSD_STAMPS
-  st[5] = stamp() - t_begin;
-#endif
-  block_sync();  // B0
-  for (int q = 0, k = 0, cc = 0; q < nstages; ++q) {  // during MFMA stage q = (tile k, chunk cc)
-    STAMP(h0);
-    // tile k's residual, during its last chunk (issued before the item reloads: the wait below
-    // for it leaves them in flight); tile k+1's addv with its first chunk
-    const bool res = RES && a.resid && cc == ncc - 1;
-    if (res) res_dma(k);
-    if (q + 1 < nstages) {
-      if (cc == ncc - 1) stage_addv(k + 1);
-      emit(smem + ((q + 1) & 1) * HALO);
-    }
-    // the residual DMA has landed (only the next stage's coefficient loads and item reloads, all
-    // issued after it, may still be in flight)
-    if (res) {  // (last stage: nothing was issued after the DMA)
-      if (q + 1 < nstages) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS + 4) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#ifdef ITSD_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-    STAMP(h1);
-    STAMP_ADD(3, h1 - h0);
-    block_sync();  // end of MFMA stage q
-    if (++cc == ncc) {
-      cc = 0;
-      ++k;
-    }
-  }
-  PWS_STAMP_OUT();
-}
 
 // ---------------------------------------------------------------------------- persistent, one MFMA wave per SIMD
 // conv3x3_gn_pws_kernel's ablations (profiles/r02_pws_ablations.txt): without the B-fragment LDS
@@ -3613,14 +2020,15 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout) {
   int segs = 0;
   if (GNW_BN / W <= H) {
     const int THs = GNW_BN / W;
-    if (H % THs == 0 && (THs + 2) * (W + 2) <= GnwCfg<1>::ITEMS * 64) segs = 1;
-  } else if (GNW_BN == 4 * H * W && (H + 2) * (W + 2) <= GnwCfg<4>::ITEMS * 16) {
+    if (H % THs == 0 && (THs + 2) * (W + 2) <= GnpCfg<32>::ITEMS * 32) segs = 1;  // p4's halo items
+  } else if (GNW_BN == 4 * H * W && (H + 2) * (W + 2) <= GnpCfg<8>::ITEMS * 8) {
     segs = 4;
   }
   const long long blocks = (long long)(M / GNW_BN) * ((Cout + CONV_BM - 1) / CONV_BM);
   return segs && (g_gn_wide == 2 || blocks >= 192) ? segs : 0;
 }
 
+#ifdef ITSD_DIAG
 // conv_pipe_wide for plain bf16 convs in whole 64-channel K-chunks whose 256-pixel tiles hold
 // whole images or whole GroupNorm statistics slots. Auto: at least 12 K-stages (short-K 1x1s
 // stay on the 2-blocks-per-CU conv_pipe) and ~one block per CU (split K below that). Returns
@@ -3651,33 +2059,69 @@ static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) 
   }
   return true;
 }
+#endif
+
+#ifdef ITSD_DIAG
+// Diagnostic builds: the compile-time ablations of conv3x3_gn_p4_kernel<32> (conv_dbg 4096 | AB << 13)
+static hipError_t launch_p4_ablation(const ConvArgs& a, dim3 gp, hipStream_t s) {
+  switch ((g_conv_dbg >> 13) & 127) {
+    case 2: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 2>), gp, dim3(512), 0, s, a); break;
+    case 4: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 4>), gp, dim3(512), 0, s, a); break;
+    case 8: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 8>), gp, dim3(512), 0, s, a); break;
+    case 16: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 16>), gp, dim3(512), 0, s, a); break;
+    case 24: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 24>), gp, dim3(512), 0, s, a); break;
+    case 10: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 10>), gp, dim3(512), 0, s, a); break;
+    case 32: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 32>), gp, dim3(512), 0, s, a); break;
+    case 64: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 64>), gp, dim3(512), 0, s, a); break;
+    case 18: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 18>), gp, dim3(512), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Diagnostic builds: the superseded 256-pixel fused convs (gn_reg = 3 pws, 2 ws, 1 reg, 0 wide)
+static bool launch_gn_wide_diag(const ConvArgs& a, int segs, hipStream_t s, hipError_t* err) {
+  const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+  const bool sq = a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
+  if (g_gn_reg >= 3 && sq) {
+    const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
+    const dim3 gp(std::min(tiles, g_num_cus));
+    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
+    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
+    else ITSD_LAUNCH(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
+  } else if (g_gn_reg == 2 && sq && a.C1 + a.C2 <= GNS_MAXC) {
+    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
+    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
+    else ITSD_LAUNCH(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
+  } else if (g_gn_reg == 1 && sq) {
+    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
+    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
+    else ITSD_LAUNCH(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
+  } else if (g_gn_reg == 0) {
+    if (segs == 1) ITSD_LAUNCH(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
+    else ITSD_LAUNCH(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
+  } else {
+    return false;
+  }
+  *err = hipGetLastError();
+  return true;
+}
+#endif
 
 template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (a.gn_coef) {
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
-        const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
-        if (g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
-            ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)))) {
+        const bool p4 = g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
+                        ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
+        if (p4) {
           // persistent, one MFMA wave per SIMD (512 threads, 256 registers a wave)
           const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
           const dim3 gp(std::min(tiles, g_num_cus));
-          if ((g_conv_dbg & 4096) && a.Wout == 32) {  // measurement builds of the W = 32 kernel only
-            switch ((g_conv_dbg >> 13) & 127) {
-              case 2: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 2>), gp, dim3(512), 0, s, a); break;
-              case 4: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 4>), gp, dim3(512), 0, s, a); break;
-              case 8: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 8>), gp, dim3(512), 0, s, a); break;
-              case 16: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 16>), gp, dim3(512), 0, s, a); break;
-              case 24: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 24>), gp, dim3(512), 0, s, a); break;
-              case 10: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 10>), gp, dim3(512), 0, s, a); break;
-              case 32: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 32>), gp, dim3(512), 0, s, a); break;
-              case 64: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 64>), gp, dim3(512), 0, s, a); break;
-              case 18: ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 18>), gp, dim3(512), 0, s, a); break;
-              default: return hipErrorInvalidValue;
-            }
-            return hipGetLastError();
-          }
+#ifdef ITSD_DIAG
+          if ((g_conv_dbg & 4096) && a.Wout == 32) return launch_p4_ablation(a, gp, s);
+#endif
           if (g_p4_m16 && a.wfrag16 && a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 0, true>), gp, dim3(512), 0, s, a);
           else if (g_p4_m16 && a.wfrag16 && a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 0, true>), gp, dim3(512), 0, s, a);
           else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p4_kernel<32>, gp, dim3(512), 0, s, a);
@@ -3685,64 +2129,10 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }
-        if (g_gn_reg >= 3 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
-            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
-          // persistent: one block per CU (160 KiB of LDS each), tiles strided over the grid
-          const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
-          const dim3 gp(std::min(tiles, g_num_cus));
-          if ((g_conv_dbg & 4096) && a.Wout == 32) {  // measurement builds of the W = 32 kernel only
-            switch ((g_conv_dbg >> 13) & 127) {
-              case 1: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 1>), gp, dim3(768), 0, s, a); break;
-              case 2: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 2>), gp, dim3(768), 0, s, a); break;
-              case 3: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 3>), gp, dim3(768), 0, s, a); break;
-              case 4: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 4>), gp, dim3(768), 0, s, a); break;
-              case 5: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 5>), gp, dim3(768), 0, s, a); break;
-              case 10: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 10>), gp, dim3(768), 0, s, a); break;
-              case 18: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 18>), gp, dim3(768), 0, s, a); break;
-              case 26: ITSD_LAUNCH((conv3x3_gn_pws_kernel<32, 26>), gp, dim3(768), 0, s, a); break;
-              default: return hipErrorInvalidValue;
-            }
-            return hipGetLastError();
-          }
-          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
-          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
-          else ITSD_LAUNCH(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
-          return hipGetLastError();
-        }
-        if (g_gn_reg == 2 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 <= GNS_MAXC &&
-            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
-          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
-          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
-          else ITSD_LAUNCH(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
-          return hipGetLastError();
-        }
-        if (g_gn_reg && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout &&
-            (a.Wout == 32 || a.Wout == 16 || a.Wout == 8)) {
-          if ((g_conv_dbg & 4096) && a.Wout == 32) {  // measurement builds of the W = 32 kernel only
-            switch ((g_conv_dbg >> 13) & 127) {
-              case 1: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 1>), gw, dim3(512), 0, s, a); break;
-              case 2: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 2>), gw, dim3(512), 0, s, a); break;
-              case 4: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 4>), gw, dim3(512), 0, s, a); break;
-              case 8: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 8>), gw, dim3(512), 0, s, a); break;
-              case 16: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 16>), gw, dim3(512), 0, s, a); break;
-              case 6: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 6>), gw, dim3(512), 0, s, a); break;
-              case 14: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 14>), gw, dim3(512), 0, s, a); break;
-              case 30: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 30>), gw, dim3(512), 0, s, a); break;
-              case 24: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 24>), gw, dim3(512), 0, s, a); break;
-              case 32: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 32>), gw, dim3(512), 0, s, a); break;
-              case 64: ITSD_LAUNCH((conv3x3_gn_reg_kernel<32, 64>), gw, dim3(512), 0, s, a); break;
-              default: return hipErrorInvalidValue;
-            }
-            return hipGetLastError();
-          }
-          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
-          else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
-          else ITSD_LAUNCH(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
-          return hipGetLastError();
-        }
-        if (segs == 1) ITSD_LAUNCH(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
-        else ITSD_LAUNCH(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
-        return hipGetLastError();
+#ifdef ITSD_DIAG
+        hipError_t de;
+        if (launch_gn_wide_diag(a, segs, s, &de)) return de;
+#endif
       }
       dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
       const int THs = std::min(a.Hout, 128 / a.Wout), segs = 128 / (THs * a.Wout);
@@ -3753,10 +2143,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   }
   constexpr int BK = 8 * (16 / (int)sizeof(T));
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+#ifdef ITSD_DIAG
   if constexpr (sizeof(T) == 2) {
     hipError_t we;
     if (conv_wide_launch(a, s, &we)) return we;
   }
+#endif
   if constexpr (sizeof(T) == 2) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)

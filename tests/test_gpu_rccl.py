@@ -47,7 +47,7 @@ def test_search_engine_over_one_rank_rccl_group_matches_no_group():
 def test_bench_under_torchrun_one_rank_nccl():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "1", "--steps", "1", "--warmup", "1", "--n", "16", "--T", "10", "--no-extras",
+           "--gpus", "1", "--steps", "1", "--warmup", "1", "--n-total", "16", "--T", "10", "--no-extras",
            "--no-cpu-baseline", "--no-live-traffic"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -73,14 +73,37 @@ def test_reference_noise_plan_order():
 
 def test_conv_tile_options():
     """The conv tile switches (itsd_set_option) accept 0 off / 1 auto / 2 whenever eligible and
-    reject other values; host-side only (no device call)."""
+    reject other values; the switches of kernels that only diagnostic builds contain (the
+    superseded 256-pixel generations, conv_pipe_wide, the compile-time ablations) fail loudly in
+    the shipped library. Host-side only (no device call)."""
     if not os.path.exists(rt.LIB_PATH):
         import __graft_entry__
 
         __graft_entry__.build()
-    for key, default in (("gn_wide", 1), ("conv_wide", 0), ("small_conv", 1)):
+    for key, default in (("gn_wide", 1), ("small_conv", 1)):
         for v in (0, 1, 2):
             rt.set_option(key, v)
         with pytest.raises(rt.ItsdError):
             rt.set_option(key, 3)
         rt.set_option(key, default)
+    rt.set_option("conv_wide", 0)
+    rt.set_option("gn_reg", 4)
+    for key, val in (("conv_wide", 1), ("gn_reg", 0), ("gn_reg", 3), ("conv_dbg", 4096 | (2 << 13))):
+        with pytest.raises(rt.ItsdError, match="diagnostic builds only"):
+            rt.set_option(key, val)
+    rt.set_option("conv_dbg", 0)
+
+
+def test_shipped_library_holds_only_product_kernels():
+    """measurement scaffolding stays out of the shipped .so -- no superseded fused-conv
+    kernel (wide / reg / ws / pws), no conv_pipe_wide, no stamps symbol (tools/build_diag.sh builds
+    them into build_diag/ instead)."""
+    if not os.path.exists(rt.LIB_PATH):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    blob = open(rt.LIB_PATH, "rb").read()
+    for name in (b"conv3x3_gn_wide_kernel", b"conv3x3_gn_reg_kernel", b"conv3x3_gn_ws_kernel",
+                 b"conv3x3_gn_pws_kernel", b"conv_pipe_wide", b"itsd_debug_stamps"):
+        assert name not in blob, name
+    assert b"conv3x3_gn_p4_kernel" in blob
