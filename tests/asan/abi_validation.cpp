@@ -57,7 +57,8 @@ int main() {
   expect("set_option gn_wide=7", itsd_set_option("gn_wide", 7), ITSD_ERR_INVALID);
   expect("set_option gn_reg=5", itsd_set_option("gn_reg", 5), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_OK);
-  expect("set_option gn_reg=3", itsd_set_option("gn_reg", 3), ITSD_OK);
+  expect("set_option gn_reg=3 (diagnostic builds only)", itsd_set_option("gn_reg", 3), ITSD_ERR_INVALID);
+  expect("set_option conv_wide=1 (diagnostic builds only)", itsd_set_option("conv_wide", 1), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
   expect("set_option p4_w=8", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
