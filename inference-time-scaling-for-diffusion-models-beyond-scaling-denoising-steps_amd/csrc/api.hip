@@ -38,6 +38,7 @@ hipError_t launch_add_int(int*, int, hipStream_t);
 hipError_t launch_run_begin(int*, int, int*, RunParams*, const RunParams&, hipStream_t);
 int g_option_gen = 0;  // bumped by every itsd_set_option: part of the step-graph cache key
 bool conv_gn_eligible(int H, int W);
+bool p5_eligible(int H, int W);
 int conv_gn_wide_segs(int H, int W, int M, int Cout);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
@@ -180,6 +181,8 @@ struct itsd_unet {
   long long graph_captures = 0;  // step graphs captured + instantiated (itsd_unet_query)
   void* zero_page = nullptr;  // 256 KiB of zeros (conv DMA source for padding, conv.hip zero_of_block)
   float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
+  int* tickets = nullptr;      // in-launch split-K counters (conv3x3_gn_p5_kernel), zero between launches
+  static constexpr long long kTicketCap = 16384;
   static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
 
   hipStream_t stream = nullptr;
@@ -402,7 +405,7 @@ struct Builder {
   bool fusable(int s1, int s2, int Cout) const {
     const Act& A = u->acts[s1];
     return u->bf16 && itsd::g_fuse_gn && A.C % 64 == 0 && (s2 < 0 || u->acts[s2].C % 64 == 0) &&
-           Cout % 128 == 0 && conv_gn_eligible(A.H, A.W);
+           Cout % 128 == 0 && (conv_gn_eligible(A.H, A.W) || p5_eligible(A.H, A.W));
   }
 
   int resblock(int x1, int x2, const std::string& p, int in_ch, int out_ch, bool attn) {
@@ -738,6 +741,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.zero = u->zero_page;
     a.splitk_ws = u->splitk_ws;
     a.splitk_cap = itsd_unet::kSplitkCap;
+    a.tickets = u->tickets;
     if (o.vt >= 0) {
       if (o.vt_from % 128 || (out.H * out.W) % 8) return fail(ITSD_ERR_INVALID, "internal: bad channel-major V split");
       a.vt_out = u->ap(o.vt);
@@ -754,7 +758,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     }
     if (o.coef != SIZE_MAX) {
       if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
-          !conv_gn_eligible(in.H, in.W) || a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
+          !(conv_gn_eligible(in.H, in.W) || p5_eligible(in.H, in.W)) || a.C1 % 64 || a.C2 % 64 || a.Cout % 128)
         return fail(ITSD_ERR_INVALID, "internal: fused GroupNorm conv on an unsupported shape");
       a.gn_coef = (const float*)(u->ws + o.coef);
     }
@@ -1026,6 +1030,16 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_w = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "p5")) {  // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto, 2 always (4x4: always)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5 in [0,2]");
+    itsd::g_p5 = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p5_split")) {  // its K slices: 0 auto (cost model), 1..16 forced
+    if (value < 0 || value > 16) return fail(ITSD_ERR_INVALID, "p5_split in [0,16]");
+    itsd::g_p5_split = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards
     itsd::g_fuse_gn = value ? 1 : 0;
     return ITSD_OK;
@@ -1084,6 +1098,8 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipMalloc(&u->zero_page, 64 * 4096 + 1024));
   HIPCHK(hipMemset(u->zero_page, 0, 64 * 4096 + 1024));
   HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
+  HIPCHK(hipMalloc(&u->tickets, itsd_unet::kTicketCap * 4));
+  HIPCHK(hipMemset(u->tickets, 0, itsd_unet::kTicketCap * 4));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -1103,6 +1119,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   hipFree(u->proj_buf); hipFree(u->cemb_table); hipFree(u->coeff1); hipFree(u->coeff2); hipFree(u->sqrt_var);
   hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->d_run); hipFree(u->x_state); hipFree(u->lab_state); hipFree(u->zero_page);
   hipFree(u->splitk_ws);
+  hipFree(u->tickets);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
   if (u->ev_out) hipEventDestroy(u->ev_out);

@@ -19,6 +19,8 @@ extern int g_p4_w;
 extern int g_p4_m16;        // 16x16x32 MFMA form of conv3x3_gn_p4_kernel (itsd_set_option "p4_m16")          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
 extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
+extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
+extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 // Census (itsd_profile_ops): the first kernel an op launches. Every launch site goes through
 // ITSD_LAUNCH, which records the kernel expression's name if none is recorded yet; the census
@@ -125,6 +127,11 @@ struct ConvArgs {
                                      // (grid.z = phase py*2+px): Hout/Wout/M/ksize/K describe the
                                      // input-grid GEMM; output rows are (2i+py, 2j+px) of a 2x grid
   int dbg;                           // g_conv_dbg (measurements only)
+  // conv3x3_gn_p5_kernel (the fused conv of the 8x8 / 4x4 levels): K split into ksplit slices
+  // (>= 1) combined in-launch by the last-arriving slice of each (tile, MFMA wave); tickets[]
+  // are zero between launches (zeroed at create, reset by each last arriver)
+  int ksplit;
+  int* tickets;
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -31,6 +31,7 @@
 namespace itsd {
 
 constexpr int CONV_BM = 128;  // couts per block
+constexpr long long kTicketCap = 16384;  // split-K tickets per UNet handle (itsd_unet::tickets)
 constexpr int CONV_BN = 128;  // pixels per block
 constexpr int ROWB = 128;     // bytes per LDS row
 constexpr int TILEB = 128 * ROWB;
@@ -51,6 +52,8 @@ int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel ch
 int g_p4_w = 7;
 int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)         // levels conv3x3_gn_p4_kernel takes under gn_reg = 4: bit 0 W = 8, 1 W = 16, 2 W = 32
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
+int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
+int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
                          // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
 
@@ -1843,6 +1846,443 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   P4_STAMP_OUT();
 }
 
+// ---------------------------------------------------------------------------- small levels, split-K persistent
+// conv3x3_gn_p5_kernel<W>: the fused GroupNorm+SiLU+conv3x3 (Model.py:170-174,179-184) of the 8x8
+// and 4x4 levels (W = 8, 4), whose tiles hold whole images. At N = 256 the 4x4 level has only
+// 4096 pixels: 128-pixel x 64-cout tiles with the whole K per block (conv_small) spend their time
+// in a 72..144-stage K loop at 9-14 % MFMA busy, and with p4's 256 x 128 tiles only 64 tiles exist.
+// Here a work item is (128-pixel tile = 8 / 2 whole images, 128 couts, K slice):
+//   * 4 MFMA waves, wave w = couts 32w .. 32w+31 x all 128 pixels (one A fragment and four B
+//     fragments per k-step: 4 v_mfma_f32_32x32x16_bf16), A streamed from wfrag into a 9-slot
+//     register ring across chunk and item boundaries, B from a double-buffered LDS halo;
+//   * 4 halo waves stage the next 64-channel chunk while the MFMA waves compute the current one
+//     (p4's software pipeline): only the tile's INTERIOR pixels are loaded (16 B a lane, one
+//     image's GroupNorm coefficients per lane), GroupNorm+SiLU'd and written; the padding rows of
+//     both halo buffers are zeroed once per launch (whole-image tiles: the same rows every item);
+//   * K split into S slices (items = tiles x S, S from a cost model so the items fill the 256
+//     CUs): each MFMA wave of a slice stores its fp32 partial (64 accumulators a lane) to a slab,
+//     releases it at agent scope and takes a ticket on a per-(tile, wave) counter; the wave that
+//     draws S-1 acquires, sums the partials in slice order 0..S-1 (deterministic whichever slice
+//     arrives last, correct for any placement over XCDs), resets the counter and runs the epilogue;
+//   * register epilogue: + bias/temb (+ CFG cond) rows staged in LDS by the halo waves + residual
+//     from HBM, one bf16 rounding, 16-B stores (permlane32 swap), and the consumer GroupNorm's
+//     statistics slots (one per image at 4x4, one per image at 8x8) by lane butterflies;
+//   * ragged batches: images past the batch load zeros (buffer-descriptor bound) and store nothing.
+// Tiles of whole images (W <= 8: NSEG = 128 / HW images, "interior" halo mode: only the images'
+// own pixels are loaded, the padding ring is zeroed once) or of TH = 128 / W rows of one image
+// (W = 16 / 32, "rows" mode: the rows above and below the tile are loaded too, masked to zero where
+// they fall outside the image; the padding columns are zeroed once).
+template <int W> struct Gp5Cfg {
+  static constexpr int HW = W * W;
+  static constexpr bool ROWS = HW > 128;
+  static constexpr int TH = ROWS ? 128 / W : W, NSEG = ROWS ? 1 : 128 / HW, W2 = W + 2, HS = (TH + 2) * W2;
+  static constexpr int HY0 = ROWS ? 0 : 1, NHY = ROWS ? TH + 2 : TH;  // halo rows loaded per segment
+  static constexpr int TPS = 256 / NSEG, RPP = TPS / 8, ITEMS = NHY * W / RPP;
+  static constexpr int HALO = ((NSEG * HS * ROWB) + 1023) & ~1023;  // one halo buffer (bytes)
+};
+constexpr int P5_RING = 9;  // A k-step slots (prefetch distance 8 k-steps = 32 MFMAs); divides 36
+constexpr int P5_BD = 3;    // B fragment buffers (reads two k-steps = 8 MFMAs ahead)
+
+template <int W>
+__global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  using Cf = Gp5Cfg<W>;
+  constexpr int HW = Cf::HW, NSEG = Cf::NSEG, W2 = Cf::W2, HS = Cf::HS, TPS = Cf::TPS, RPP = Cf::RPP;
+  constexpr int ITEMS = Cf::ITEMS, HALO = Cf::HALO, TH = Cf::TH, HY0 = Cf::HY0, NHY = Cf::NHY;
+  constexpr int SPX = TH * W;  // pixels of one segment
+  static_assert(NSEG * SPX == 128 && ITEMS * RPP == NHY * W && ITEMS <= 31 && 36 % P5_RING == 0, "p5 geometry");
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + 2 * NSEG * CONV_BM * 4];
+  float* const addv = (float*)(smem + 2 * HALO);  // [item parity][image of the tile][128 couts]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
+  const int nimg = a.M / HW, nTP = Cf::ROWS ? a.M / 128 : (nimg + NSEG - 1) / NSEG;
+  const int nTC = a.Cout / CONV_BM, S = a.ksplit;
+  const int NI = nTP * nTC * S;
+  const int G = gridDim.x, b = blockIdx.x;
+  // XCD-aware: the dispatcher deals block ids round-robin over the 8 XCDs; XCD x takes the
+  // contiguous logical range, in which items sharing a (cout tile, slice) -- its weights -- are adjacent
+  const int bl = (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+  const int nit = bl < NI ? (NI - 1 - bl) / G + 1 : 0;
+  if (nit == 0) return;  // (the host launches gridDim.x <= items)
+  // item k of this block -> pixel tile tp (fastest), K slice z, cout tile tc
+  auto item_of = [&](int k, int& tp, int& tc, int& z) {
+    const int L = bl + k * G;
+    tp = L % nTP;
+    const int r = L / nTP;
+    z = r % S;
+    tc = r / S;
+  };
+  auto chunk_lo = [&](int z) { return (nch * z) / S; };
+  auto block_sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if (wid < 4) {
+    // ================================================================ MFMA waves
+    const int rl = lane & 31, hh = lane >> 5;
+    int hb[4];  // halo row of this lane's pixel (tap 0, 0) in each 32-pixel block
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = j * 32 + rl, seg = pl / SPX, rem = pl - seg * SPX, y = rem / W;
+      hb[j] = seg * HS + y * W2 + (rem - y * W);
+    }
+    const size_t ablk = (size_t)(9 * kpt) * 1024;  // one 32-cout block of fragments
+    auto abase = [&](int tc, int cc) {
+      return (const char*)a.wfrag + (size_t)(tc * 4 + wid) * ablk + (size_t)cc * 4 * 1024 + lane * 16;
+    };
+    auto load_a = [&](const char* base, int st, u32x4& dst) __attribute__((always_inline)) {
+      dst = *(const u32x4*)(base + (size_t)((st >> 2) * kpt + (st & 3)) * 1024);
+    };
+    f32x16 acc[4];
+    u32x4 ra[P5_RING];
+    {
+      int tp, tc, z;
+      item_of(0, tp, tc, z);
+      const char* ab0 = abase(tc, chunk_lo(z));
+#pragma unroll
+      for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
+    }
+    block_sync();  // B0: stage 0 staged
+    int q = 0;
+    for (int k = 0; k < nit; ++k) {
+      int tp, tc, z;
+      item_of(k, tp, tc, z);
+      const int c0 = chunk_lo(z), c1 = chunk_lo(z + 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+      const char* nitem = nullptr;  // the next item's first chunk (A prefetch across the item boundary)
+      if (k + 1 < nit) {
+        int tp2, tc2, z2;
+        item_of(k + 1, tp2, tc2, z2);
+        nitem = abase(tc2, chunk_lo(z2));
+      }
+      for (int cc = c0; cc < c1; ++cc, ++q) {
+        const char* hcur = smem + (q & 1) * HALO;
+        const char* cb = abase(tc, cc);
+        const char* nb = cc + 1 < c1 ? abase(tc, cc + 1) : (nitem ? nitem : cb);
+        int tb[4];
+        bf16x8 fb[P5_BD][4];
+        auto rd = [&](int st, int buf) __attribute__((always_inline)) {
+          if ((st & 3) == 0) {
+            const int tap = st >> 2, ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              int h = hb[j] + ky * W2 + kx;
+              asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
+              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 3) << 5)));
+        };
+#pragma unroll
+        for (int s0 = 0; s0 < P5_BD - 1; ++s0) rd(s0, s0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int step = 0; step < 36; ++step) {
+          const int pf = step + P5_RING - 1;
+          if (pf < 36) load_a(cb, pf, ra[pf % P5_RING]);
+          else load_a(nb, pf - 36, ra[pf % P5_RING]);
+          if (step + P5_BD - 1 < 36) rd(step + P5_BD - 1, (step + P5_BD - 1) % P5_BD);
+          __builtin_amdgcn_sched_barrier(0);
+          const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % P5_RING]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc[j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
+      }
+      // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines
+      const int tile = tc * nTP + tp;
+      if (S > 1) {
+        // Guideline 16's R1 hand-off, per wave: the partial is stored write-through (sc1), the wave
+        // drains its stores, then adds to its (tile, wave) counter; the wave whose add returns S-1 reads
+        // every partial with sc1 loads (past its own L1) -- no release / acquire fence, whose L2
+        // write-back / L1 invalidate cost ~2-7 us per episode (MI355X_MICROARCH.md, visibility table)
+        const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+            a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
+        const uint32_t wbase = (uint32_t)(((size_t)tile * S * 4 + wid) * 4096 * 4) + lane * 16;
+        const uint32_t zstride = 4 * 4096 * 4;  // bytes between the slices of one (tile, wave)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]), __float_as_uint(acc[j][4 * g + 2]),
+                      __float_as_uint(acc[j][4 * g + 3])},
+                slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(a.tickets + tile * 4 + wid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (old != S - 1) continue;  // another slice finishes this tile
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the add)
+        if (lane == 0) __hip_atomic_store(a.tickets + tile * 4 + wid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every slice's partial (this one's included), summed in slice order
+        for (int sl = 0; sl < S; ++sl) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(slab, wbase + sl * zstride + (j * 4 + g) * 1024, 0, 16);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc[j][4 * g + e] = sl == 0 ? __uint_as_float(v[e]) : acc[j][4 * g + e] + __uint_as_float(v[e]);
+            }
+        }
+      }
+      // ---- epilogue: out = acc + addv + residual (lane: pixel 32j + rl, couts 32w + 8g + 4hh + e)
+      const int tileP = tp * 128, tileC = tc * CONV_BM;
+      const float* av = addv + (k & 1) * NSEG * CONV_BM + wid * 32 + 4 * hh;
+      const bool has_res = a.resid != nullptr;
+      float s16[16], q16[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pl = j * 32 + rl, seg = pl / SPX;
+        const bool live = Cf::ROWS ? tp * 128 < a.M : tp * NSEG + seg < nimg;
+        const float* avj = av + seg * CONV_BM;
+        uint32_t wv[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = wid * 32 + 8 * g + 4 * hh;
+          const f32x4 ad = *(const f32x4*)(avj + 8 * g);
+          const T* rp = has_res && live ? (const T*)a.resid + (size_t)(tileP + pl) * a.Cout + tileC + c
+                                        : (const T*)zero_of_block<T>(a);
+          uint2 rr = *(const uint2*)rp;
+          if (!has_res) rr = uint2{0u, 0u};
+          float v[4];
+          v[0] = acc[j][4 * g + 0] + ad[0] + __uint_as_float(rr.x << 16);
+          v[1] = acc[j][4 * g + 1] + ad[1] + __uint_as_float(rr.x & 0xffff0000u);
+          v[2] = acc[j][4 * g + 2] + ad[2] + __uint_as_float(rr.y << 16);
+          v[3] = acc[j][4 * g + 3] + ad[3] + __uint_as_float(rr.y & 0xffff0000u);
+          const T b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
+          wv[g][0] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+          wv[g][1] = (uint32_t)b2 | ((uint32_t)b3 << 16);
+          const float m = live ? 1.0f : 0.0f;
+          const float r0 = bf2f(b0) * m, r1 = bf2f(b1) * m, r2 = bf2f(b2) * m, r3 = bf2f(b3) * m;
+          s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
+          s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
+          s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
+          s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
+        }
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+          u32x4 o;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+            o[d] = sw[0];
+            o[2 + d] = sw[1];
+          }
+          const int c8 = wid * 32 + 8 * (gp + hh);
+          if (live) *(u32x4*)((T*)a.out + (size_t)(tileP + pl) * a.Cout + tileC + c8) = o;
+        }
+        // consumer GroupNorm statistics: one slot per image (W = 8: j-blocks {0,1} / {2,3};
+        // W = 4: lanes 0-15 / 16-31 of each j-block), one per 128-pixel tile (W >= 16: all four)
+        if (a.stats && (W == 4 || (W == 8 && (j & 1)) || j == 3)) {
+          float v[32];
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            v[e] = s16[e];
+            v[16 + e] = q16[e];
+          }
+          auto xchg = [](float x, auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const int xi = __builtin_bit_cast(int, x);
+            int r;
+            if constexpr (w == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+            else if constexpr (w == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+            else if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+            else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (w << 10));
+            return __builtin_bit_cast(float, r);
+          };
+          // halve(d, n): lanes with bit d of rl keep the upper n/2 values, each summed with its partner's
+          auto halve = [&](auto wc, auto nc) {
+            constexpr int d = decltype(wc)::value, n = decltype(nc)::value;
+            const bool up = (rl & d) != 0;
+#pragma unroll
+            for (int ii = 0; ii < n / 2; ++ii) {
+              const float lo = v[ii], hi = v[ii + n / 2];
+              v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+            }
+          };
+          if constexpr (W >= 8) {  // 64-pixel slot (W = 8: 2 j-blocks) / 128-pixel slot: one value a lane
+            halve(std::integral_constant<int, 16>{}, std::integral_constant<int, 32>{});
+            halve(std::integral_constant<int, 8>{}, std::integral_constant<int, 16>{});
+            halve(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
+            halve(std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
+            halve(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
+            const long long slot = W == 8 ? tp * NSEG + (j >> 1) : tp;  // = global pixel / stat_slot_px
+            const int e = rl & 15, co = wid * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+            if (slot * (W == 8 ? 64 : 128) < a.M) a.stats[(slot * 2 + (rl >> 4)) * a.Cout + tileC + co] = v[0];
+          } else {  // 16-pixel slot = 16 lanes: two values a lane, idx = 2 (rl & 15) + {0, 1}
+            halve(std::integral_constant<int, 8>{}, std::integral_constant<int, 32>{});
+            halve(std::integral_constant<int, 4>{}, std::integral_constant<int, 16>{});
+            halve(std::integral_constant<int, 2>{}, std::integral_constant<int, 8>{});
+            halve(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+            const int img = tp * NSEG + 2 * j + (rl >> 4);
+            const int m = rl & 7, co = wid * 32 + 8 * (m >> 1) + 4 * hh + 2 * (m & 1);
+            if (img < nimg) *(float2*)(a.stats + ((long long)img * 2 + ((rl >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+        }
+      }
+    }
+    return;
+  }
+
+  // ================================================================== halo waves
+  // thread tt: 8 channels (16 B unit lch) of interior pixels (lt >> 3) + RPP j of image segment sg
+  const int tt = tid - 256, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
+  int lds[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const int r = (lt >> 3) + RPP * j, hy = HY0 + r / W, x = r - (r / W) * W;
+    const int hrow = sg * HS + hy * W2 + (x + 1);
+    lds[j] = hrow * ROWB + ((lch ^ ((hrow >> 1) & 7)) << 4);
+  }
+  // the halo rows no item writes (the padding columns; interior mode: also the top and bottom rows)
+  // of both buffers: zeroed once (item writes never touch them, so no ordering against the first
+  // emit is needed; the MFMA waves read after B0)
+  for (int u = tt; u < 2 * NSEG * HS * 8; u += 256) {
+    const int row = (u >> 3) % (NSEG * HS), buf = (u >> 3) / (NSEG * HS), r = row % HS, y = r / W2, x = r - y * W2;
+    if (x == 0 || x == W2 - 1 || (!Cf::ROWS && (y == 0 || y == TH + 1)))
+      *(u32x4*)(smem + buf * HALO + row * ROWB + ((u & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
+  }
+  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
+  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
+  struct Src {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t rowb, so;
+  };
+  auto src_of = [&](int cc) __attribute__((always_inline)) {
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    Src c;
+    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0, s1 ? nrec1 : nrec2, 0x00020000);
+    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
+    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
+    return c;
+  };
+  // the stage sequence of this block: (item k, chunk cc); E = the next stage to emit (its data in
+  // h, its prescaled coefficients in c, its image mask in zm), L = the stage after it
+  u32x4 h[ITEMS];
+  f32x4 c[4], cn[4];
+  uint32_t zm = 0, zmn = 0;      // bit j: item j of the emitted / loaded stage is real input (else zero)
+  int kL = 0, ccL = 0, c1L = 0;  // the stage being loaded and its item's chunk end
+  int pix0 = 0;                  // global pixel of this thread's item 0 of the loaded stage (r = lt >> 3)
+  const float* cbase = a.gn_coef;
+  auto open_item = [&](int k) __attribute__((always_inline)) {  // geometry of item k (as the loaded stage)
+    int tp, tc, z;
+    item_of(k, tp, tc, z);
+    ccL = chunk_lo(z);
+    c1L = chunk_lo(z + 1);
+    const int img = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sg;
+    const int y0 = Cf::ROWS ? ((tp * 128) % HW) / W : 0;  // the tile's first image row
+    const int imgc = img < nimg ? img : nimg - 1;
+    pix0 = img * HW + (y0 - 1 + HY0) * W + (lt >> 3);
+    zmn = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int y = y0 - 1 + HY0 + ((lt >> 3) + RPP * j) / W;
+      zmn |= (uint32_t)(img < nimg && y >= 0 && y < W) << j;  // (square images: H = W)
+    }
+    cbase = a.gn_coef + ((size_t)imgc * (Cin / 8) + lch) * 16;
+  };
+  auto load_stage = [&]() __attribute__((always_inline)) {  // coefficients + items of stage L
+    const f32x4* cp = (const f32x4*)(cbase + ccL * 128);
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) cn[qq] = cp[qq];
+  };
+  auto prescale = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) c[qq][e] = cn[qq][e] * GN_L2E;
+    zm = zmn;
+  };
+  bool more = true;  // a stage L exists
+  auto advance = [&]() __attribute__((always_inline)) {  // L <- the stage after L
+    if (++ccL == c1L) {
+      if (++kL < nit) open_item(kL);
+      else more = false;
+    }
+  };
+  // emit: transform stage E (h, c, zm) into hbuf, reloading each item's register with stage L's
+  auto emit = [&](char* hbuf) __attribute__((always_inline)) {
+    const bool live = more;
+    if (live) load_stage();
+    const Src nx = src_of(live ? ccL : 0);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      uint32_t yw[4];
+      const uint32_t zj = (uint32_t)__builtin_amdgcn_sbfe((int)zm, j, 1);  // 0 (padding) or ~0
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+        gn_silu_x4(h[j][2 * hf], h[j][2 * hf + 1], c[hf][0], c[hf][1], c[hf][2], c[hf][3], c[2 + hf][0],
+                   c[2 + hf][1], c[2 + hf][2], c[2 + hf][3], zj, yw[2 * hf], yw[2 * hf + 1]);
+      *(u32x4*)(hbuf + lds[j]) = u32x4{yw[0], yw[1], yw[2], yw[3]};
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t pix = live && ((zmn >> j) & 1) ? (uint32_t)(pix0 + RPP * j) : 0u;
+      h[j] = __builtin_amdgcn_raw_buffer_load_b128(nx.rs, __umul24(pix, nx.rowb) + lch * 16, nx.so, 0);
+    }
+    prescale();
+    if (live) advance();
+  };
+  auto stage_addv = [&](int k) {  // bias (+ time / class embedding) of item k's images x couts
+    int tp, tc, z;
+    item_of(k, tp, tc, z);
+    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+    for (int it = tt; it < NSEG * CONV_BM; it += 256) {
+      const int il = it / CONV_BM, cl = it % CONV_BM, co = tc * CONV_BM + cl;
+      const int img = min(Cf::ROWS ? (tp * 128) / HW : tp * NSEG + il, nimg - 1);
+      float v = a.bias[co];
+      if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
+      if (a.cemb) {
+        int lab = 0;
+        if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
+        v += a.cemb[(long long)lab * a.cemb_row_stride + co];
+      }
+      addv[(k & 1) * NSEG * CONV_BM + it] = v;
+    }
+  };
+  // prologue: stage 0 into buffer 0 (stage 1 loading)
+  open_item(0);
+  load_stage();
+  {
+    const Src s0 = src_of(ccL);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      h[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          s0.rs, __umul24(((zmn >> j) & 1) ? (uint32_t)(pix0 + RPP * j) : 0u, s0.rowb) + lch * 16, s0.so, 0);
+  }
+  prescale();
+  advance();
+  emit(smem);
+  block_sync();  // B0
+  // during MFMA stage q (item k, chunk cc): stage item k's addv with its first chunk, emit stage q+1
+  int q = 0;
+  for (int k = 0; k < nit; ++k) {
+    int tp, tc, z;
+    item_of(k, tp, tc, z);
+    const int c0 = chunk_lo(z), c1 = chunk_lo(z + 1);
+    for (int cc = c0; cc < c1; ++cc, ++q) {
+      if (cc == c0) stage_addv(k);
+      if (!(k + 1 == nit && cc + 1 == c1)) emit(smem + ((q + 1) & 1) * HALO);
+      block_sync();  // end of MFMA stage q
+    }
+  }
+}
+
 // GroupNorm finalize for the fused conv (the statistics half of gn_apply_kernel): per
 // image the group mean / rstd in fp64 from the producers' slabs, then per channel
 // a = rstd*gamma, b = beta - mean*a as coef[img][C/8][a0..a7, b0..b7].
@@ -2061,6 +2501,42 @@ static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) 
 }
 #endif
 
+// conv3x3_gn_p5_kernel: levels whose 128-pixel tiles hold whole images
+bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 || W == 32); }
+
+// K slices of a p5 launch: the S minimising ceil(items / CUs) x (chunks per slice + ~1.5 chunks of
+// prologue / epilogue / combine), bounded by the slab and ticket capacities
+static int p5_split(const ConvArgs& a, int tiles, int nch) {
+  int S = 1;
+  if (g_p5_split > 0) {
+    S = std::min(g_p5_split, nch);
+  } else {
+    double best = 1e30;
+    for (int s = 1; s <= std::min(nch, 16); ++s) {
+      const double waves = std::ceil((double)tiles * s / g_num_cus);
+      const double cost = waves * (std::ceil((double)nch / s) + 1.5);
+      if (cost < best - 1e-9) { best = cost; S = s; }
+    }
+  }
+  while (S > 1 && ((long long)tiles * S * 4 * 4096 > a.splitk_cap || (long long)tiles * 4 > kTicketCap)) --S;
+  return S;
+}
+
+static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
+  ConvArgs a = a0;
+  const int HW = a.Hout * a.Wout, nimg = a.M / HW;
+  const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
+  const int tiles = ptiles * (a.Cout / CONV_BM), nch = (a.C1 + a.C2) / 64;
+  a.ksplit = (a.splitk_ws && a.tickets) ? p5_split(a, tiles, nch) : 1;
+  const int items = tiles * a.ksplit;
+  const dim3 g(std::min(items, g_num_cus));
+  if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);
+  else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p5_kernel<16>, g, dim3(512), 0, s, a);
+  else if (a.Wout == 8) ITSD_LAUNCH(conv3x3_gn_p5_kernel<8>, g, dim3(512), 0, s, a);
+  else ITSD_LAUNCH(conv3x3_gn_p5_kernel<4>, g, dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
 #ifdef ITSD_DIAG
 // Diagnostic builds: the compile-time ablations of conv3x3_gn_p4_kernel<32> (conv_dbg 4096 | AB << 13)
 static hipError_t launch_p4_ablation(const ConvArgs& a, dim3 gp, hipStream_t s) {
@@ -2112,6 +2588,11 @@ template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (a.gn_coef) {
+      if (a.wfrag && a.Cout % CONV_BM == 0 && a.C1 % 64 == 0 && a.C2 % 64 == 0 && p5_eligible(a.Hout, a.Wout)) {
+        // the 4x4 level always (no other fused kernel holds it); the others where p4 under-fills the chip
+        const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
+        if (a.Wout == 4 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192)) return launch_p5(a, s);
+      }
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
         const bool p4 = g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
                         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
