@@ -28,6 +28,9 @@ template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
 template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
 template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
 bool attn_flash_ok(int S, int C);
+bool attn_block_ok(int S, int C);
+hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
+int g_attn_fuse = 1;  // fused AttnBlock kernel where it applies (itsd_set_option "attn_fuse", read at create)
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
 hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
@@ -88,7 +91,8 @@ struct Act {
   int spi = 0;              // its slots per image (0: H*W / stat_slot_px(H*W); sub-pixel outputs: stat_spi)
 };
 
-enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF };
+enum OpKind { OP_GN, OP_CONV, OP_ATTN, OP_GNCOEF, OP_ATTNBLOCK };
+constexpr int kCensusAttnBlock = 7;  // census kind of OP_ATTNBLOCK (runtime.py "attnblock")
 constexpr int kCensusConvGN = 4;  // census kind of a fused GroupNorm+SiLU conv (conv3x3_gn_kernel)
 constexpr int kCensusConvGNW = 5;   // ... run as conv3x3_gn_wide_kernel<1>
 constexpr int kCensusConvGNW4 = 6;  // ... run as conv3x3_gn_wide_kernel<4>
@@ -112,6 +116,7 @@ struct Op {
   int S = 0, C = 0;
   int vt = -1, vt_from = 0;  // channel-major V buffer (conv: couts >= vt_from go there; attn: reads it)
   size_t coef = SIZE_MAX;    // GNCOEF: output; CONV: GroupNorm+SiLU coefficients of the input (fused conv)
+  size_t wt2 = 0, bias2 = 0;  // ATTNBLOCK: the proj matrix (fragment-packed) and bias; wt / bias: q|k|v
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -433,6 +438,35 @@ struct Builder {
     if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
     if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
     else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
+    if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch)) {
+      // the whole AttnBlock in one launch (kernels.hip attn_block_kernel)
+      const std::string a = p + ".attn";
+      const int64_t cc = (int64_t)out_ch * out_ch;
+      std::vector<float> wcat((size_t)3 * cc, 0.f);
+      const float* wq = get(a + ".proj_q.weight", cc);
+      const float* wk = get(a + ".proj_k.weight", cc);
+      const float* wv = get(a + ".proj_v.weight", cc);
+      if (wq && wk && wv) {
+        std::memcpy(wcat.data(), wq, cc * 4);
+        std::memcpy(wcat.data() + cc, wk, cc * 4);
+        std::memcpy(wcat.data() + 2 * cc, wv, cc * 4);
+      }
+      Op ab;
+      ab.kind = OP_ATTNBLOCK;
+      ab.src1 = o;
+      ab.gamma = f32(a + ".group_norm.weight", out_ch);
+      ab.beta = f32(a + ".group_norm.bias", out_ch);
+      ab.wt = pack_frag(wcat.data(), 3 * out_ch, out_ch, 1);
+      ab.bias = concat_f32({get(a + ".proj_q.bias", out_ch), get(a + ".proj_k.bias", out_ch),
+                            get(a + ".proj_v.bias", out_ch)}, out_ch);
+      ab.wt2 = pack_frag(get(a + ".proj.weight", cc), out_ch, out_ch, 1);
+      ab.bias2 = f32(a + ".proj.bias", out_ch);
+      ab.S = H * W;
+      ab.C = out_ch;
+      ab.dst = act(H, W, out_ch);
+      u->ops.push_back(ab);
+      return ab.dst;
+    }
     if (attn) {
       const std::string a = p + ".attn";
       int ga = act(H, W, out_ch);
@@ -627,7 +661,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   {
     std::vector<int> need;
     for (const Op& o : u->ops)
-      if (o.kind == OP_GN || o.kind == OP_GNCOEF) {
+      if (o.kind == OP_GN || o.kind == OP_GNCOEF || o.kind == OP_ATTNBLOCK) {
         need.push_back(o.src1);
         if (o.src2 >= 0) need.push_back(o.src2);
       }
@@ -642,7 +676,7 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
       A.stats = b.ws_off;
       b.ws_off = (b.ws_off + slots * 2 * A.C * 4 + 255) & ~(size_t)255;
       bool produced = (id == u->head_out);
-      for (const Op& o : u->ops) produced |= (o.kind == OP_CONV && o.dst == id);
+      for (const Op& o : u->ops) produced |= ((o.kind == OP_CONV || o.kind == OP_ATTNBLOCK) && o.dst == id);
       if (!produced) return fail(ITSD_ERR_INVALID, "internal: GroupNorm input without a statistics producer");
     }
   }
@@ -768,6 +802,24 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
         return fail(ITSD_ERR_INVALID, "conv channels must be multiples of " + std::to_string(epc));
     }
     e = u->bf16 ? launch_conv<bf16_t>(a, s) : launch_conv<float>(a, s);
+  } else if (o.kind == OP_ATTNBLOCK) {
+    AttnBlockArgs a{};
+    const Act& in = u->acts[o.src1];
+    const Act& out = u->acts[o.dst];
+    a.x = (const bf16_t*)u->ap(o.src1);
+    a.st = (const float*)(u->ws + in.stats);
+    a.spi = stat_spi(in.H * in.W, in.spi);
+    a.gamma = u->wp(o.gamma);
+    a.beta = u->wp(o.beta);
+    a.wqkv = (const bf16_t*)(u->wdev + o.wt);
+    a.bqkv = u->wp(o.bias);
+    a.wp = (const bf16_t*)(u->wdev + o.wt2);
+    a.bp = u->wp(o.bias2);
+    a.out = (bf16_t*)u->ap(o.dst);
+    a.out_stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
+    a.scale = (float)std::pow((double)o.C, -0.5);
+    a.n = c.nb;
+    e = launch_attn_block(a, o.C, s);
   } else {
     AttnArgs a{};
     a.qkv = u->ap(o.src1);
@@ -787,6 +839,8 @@ double op_flops(const itsd_unet* u, const Op& o, int nb) {
     return 2.0 * nb * out.H * out.W * (double)o.Cout * (o.subpix ? o.K * 4 / 9 : o.K);
   }
   if (o.kind == OP_ATTN) return 2.0 * 2.0 * nb * (double)o.S * o.S * o.C;
+  if (o.kind == OP_ATTNBLOCK)  // q|k|v and proj projections + the two attention products
+    return 2.0 * nb * (double)o.S * (4.0 * o.C * o.C) + 2.0 * 2.0 * nb * (double)o.S * o.S * o.C;
   return 0.0;
 }
 
@@ -827,7 +881,7 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
   }));
   // census kinds: OpKind, and kCensusConvGN for the fused GroupNorm+SiLU convs
   for (const Op& o : u->ops) {
-    int kind = (int)o.kind;
+    int kind = o.kind == OP_ATTNBLOCK ? kCensusAttnBlock : (int)o.kind;
     if (o.kind == OP_CONV && o.coef != SIZE_MAX) {
       const Act& out = u->acts[o.dst];
       const int segs = u->bf16 ? conv_gn_wide_segs(out.H, out.W, c.nb * out.H * out.W, o.Cout) : 0;
@@ -1038,6 +1092,10 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p5_split")) {  // its K slices: 0 auto (cost model), 1..16 forced
     if (value < 0 || value > 16) return fail(ITSD_ERR_INVALID, "p5_split in [0,16]");
     itsd::g_p5_split = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards
+    itsd::g_attn_fuse = value ? 1 : 0;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards

@@ -161,6 +161,22 @@ struct AttnArgs {
   float scale;
 };
 
+// Fused AttnBlock at S = 64 (kernels.hip attn_block_kernel).
+struct AttnBlockArgs {
+  const bf16_t* x;        // [n][64][C] NHWC (the ResBlock output)
+  const float* st;        // its GroupNorm statistics slab [n * spi][2][C]
+  int spi;                // statistics slots per image
+  const float* gamma; const float* beta;
+  const bf16_t* wqkv;     // [3C/32][C/16][64][8]: q rows, k rows, v rows
+  const float* bqkv;      // [3C]
+  const bf16_t* wp;       // [C/32][C/16][64][8]
+  const float* bp;        // [C]
+  bf16_t* out;            // [n][64][C]
+  float* out_stats;       // [n][2][C] (one slot per image) or null
+  float scale;            // C^-0.5
+  int n;
+};
+
 struct HeadArgs {
   const float* x;       // NCHW fp32 [n][3][H][W]
   const float* w;       // [Cout][3][3][3] fp32 (reference layout)

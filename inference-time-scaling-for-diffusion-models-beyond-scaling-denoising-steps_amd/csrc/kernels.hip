@@ -4,6 +4,8 @@
 // verifiers, and the counter-based Philox normal generator.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace itsd {
@@ -310,6 +312,384 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
     }
   }
 }
+
+// ---------------------------------------------------------------------------- fused AttnBlock, S = 64
+// attn_block_kernel<C>: one image's whole AttnBlock (Model.py:145-164) per block -- Arch A's 8x8
+// level (S = 64 tokens, C = 384), where the unfused path ran a materialised GroupNorm, the q|k|v
+// 1x1 conv (C x 3C over 64 tokens), the attention kernel and the proj conv as four launches with
+// three HBM round trips, 2 % of MFMA peak in the attention itself. Here:
+//   0. GroupNorm(32, C) of x: group mean / rstd in fp64 from the producer's statistics slab, x
+//      staged as hn = bf16(x a + b) in LDS ([token][C], 16-B chunks XOR-swizzled by token & 15);
+//   1. V^T = (hn Wv^T + bv)^T -> LDS [C][64] (D[token][c] with Wv fragments as the B operand, so a
+//      lane holds 4 consecutive tokens of one channel: 8-B channel-major stores);
+//   2. per 128-channel chunk: Q_c, K_c = hn W^T + b (D[c][token]: weights as A) -> LDS [64][128],
+//      and the scores S^T[key][query] += K_c Q_c^T accumulate in registers (one 32x32 tile a wave);
+//   3. softmax over keys in fp32 (S^T staged through LDS, 4 lanes a query), P [query][key] bf16;
+//   4. O^T = V^T P^T (both operands from LDS) -> O [token][C] bf16 in LDS (hn's space);
+//   5. out = x + O Wp^T + bp, one bf16 rounding, 16-B stores (permlane32 swap), and the consumer
+//      GroupNorm statistics of out (one slot per image) by lane butterflies.
+// Roundings as the unfused path: hn, q / k / v, P and O in bf16, fp32 accumulation.
+// 4 waves; weights (fragment-packed [Cout/32][K/16][64][8] bf16) stream from L2 into VGPRs with a
+// 4-k-step prefetch; one block per image.
+
+template <int C>
+__global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128;
+  static_assert(C % 128 == 0, "C");
+  constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256;
+  __shared__ __attribute__((aligned(16))) char sm[R_GS + 32 * 2 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int img = blockIdx.x;
+  const bf16_t* x = a.x + (size_t)img * S * C;
+  // [row][C] bf16 image, 16-B chunk ch of row r at (ch ^ (r & 15))
+  auto rowc = [](int r, int ch, int rowbytes) { return r * rowbytes + ((ch ^ (r & 15)) << 4); };
+  // [row][64] bf16 image (128-B rows), chunk ch of row r at ch ^ ((r >> 1) & 7)
+  auto row64 = [](int r, int ch) { return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4); };
+  auto frag = [&](const bf16_t* W, int cb, int st) -> const bf16x8* {
+    return (const bf16x8*)((const char*)W + ((size_t)cb * KS + st) * 1024 + lane * 16);
+  };
+  // ---- 0. GroupNorm statistics -> (mean, rstd) per group; hn
+  float* gs = (float*)(sm + R_GS);
+  {
+    const int g = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
+    double s = 0.0, q = 0.0;
+    for (int k = l8; k < n_it; k += 8) {
+      const int c = g * gsz + k / a.spi;
+      const long long sl = (long long)img * a.spi + k % a.spi;
+      s += (double)a.st[(sl * 2) * C + c];
+      q += (double)a.st[(sl * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      q += __shfl_xor(q, o, 64);
+    }
+    if (l8 == 0) {
+      const double E = (double)gsz * S, mean = s / E;
+      double var = q / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      gs[2 * g] = (float)mean;
+      gs[2 * g + 1] = (float)(1.0 / sqrt(var + 1e-5));
+    }
+  }
+  __syncthreads();
+  for (int u = tid; u < S * (C / 8); u += 256) {
+    const int t = u / (C / 8), ch = u - t * (C / 8), c0 = ch * 8;
+    const u32x4 v = *(const u32x4*)(x + (size_t)t * C + c0);
+    uint32_t o[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      float y[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = c0 + 2 * e2 + h2, g = c / (C / 32);  // (an 8-channel chunk may straddle two groups)
+        const float mean = gs[2 * g], rstd = gs[2 * g + 1];
+        const float sc = rstd * a.gamma[c];
+        const float xv = __uint_as_float(h2 ? (v[e2] & 0xffff0000u) : (v[e2] << 16));
+        y[h2] = xv * sc + (a.beta[c] - mean * sc);
+      }
+      o[e2] = pk_bf16(y[0], y[1]);
+    }
+    *(u32x4*)(sm + rowc(t, ch, C * 2)) = u32x4{o[0], o[1], o[2], o[3]};
+  }
+  __syncthreads();
+  // hn fragment of (token row r, k-step st): lane (rl, hh) reads channels 16 st + 8 hh ..
+  auto hn_frag = [&](int r, int st) { return *(const bf16x8*)(sm + rowc(r, 2 * st + hh, C * 2)); };
+
+  // ---- 1. V^T: D[token][c] = hn Wv^T; wave w owns channel blocks CBW w .. (x 2 token blocks)
+  {
+    f32x16 acc[2][CBW];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int b = 0; b < CBW; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][b][r] = 0.f;
+    constexpr int PF = 4;
+    bf16x8 bw[PF][CBW];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) bw[p][b] = *frag(a.wqkv, 2 * CB + CBW * w + b, p);
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      bf16x8 cur[CBW];
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) cur[b] = bw[st % PF][b];
+      if (st + PF < KS)
+#pragma unroll
+        for (int b = 0; b < CBW; ++b) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + CBW * w + b, st + PF);
+      const bf16x8 h0 = hn_frag(rl, st), h1 = hn_frag(32 + rl, st);
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) {
+        acc[0][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur[b], acc[0][b], 0, 0, 0);
+        acc[1][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, cur[b], acc[1][b], 0, 0, 0);
+      }
+    }
+    // lane: channel c = 32 cb + rl (column), tokens 32 i + 8 g + 4 hh + e (rows)
+#pragma unroll
+    for (int b = 0; b < CBW; ++b) {
+      const int c = 32 * (CBW * w + b) + rl;
+      const float bv = a.bqkv[2 * C + c];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(uint2*)(sm + R_VT + row64(c, 4 * i + g) + 8 * hh) =
+              uint2{pk_bf16(acc[i][b][4 * g] + bv, acc[i][b][4 * g + 1] + bv),
+                    pk_bf16(acc[i][b][4 * g + 2] + bv, acc[i][b][4 * g + 3] + bv)};
+    }
+  }
+  // ---- 2. Q_c, K_c per 128-channel chunk; S^T (keys x queries) tile (w >> 1, w & 1) in registers
+  f32x16 sacc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+  char* const Qc = sm + R_QK;
+  char* const Kc = sm + R_QK + S * 256;
+  for (int ch = 0; ch < NCH; ++ch) {
+    {
+      f32x16 aq[2], ak[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) aq[j][r] = ak[j][r] = 0.f;
+      const int cbq = 4 * ch + w, cbk = CB + 4 * ch + w;
+      constexpr int PF = 4;
+      bf16x8 wq[PF], wk[PF];
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        wq[p] = *frag(a.wqkv, cbq, p);
+        wk[p] = *frag(a.wqkv, cbk, p);
+      }
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const bf16x8 q_ = wq[st % PF], k_ = wk[st % PF];
+        if (st + PF < KS) {
+          wq[st % PF] = *frag(a.wqkv, cbq, st + PF);
+          wk[st % PF] = *frag(a.wqkv, cbk, st + PF);
+        }
+        const bf16x8 h0 = hn_frag(rl, st), h1 = hn_frag(32 + rl, st);
+        aq[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h0, aq[0], 0, 0, 0);
+        aq[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h1, aq[1], 0, 0, 0);
+        ak[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h0, ak[0], 0, 0, 0);
+        ak[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h1, ak[1], 0, 0, 0);
+      }
+      // lane: token 32 j + rl (column), channels 32 w + 8 g + 4 hh + e of the chunk (rows)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = 32 * j + rl;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int cq = 128 * ch + 32 * w + 8 * g + 4 * hh;
+          const f32x4 bq = *(const f32x4*)(a.bqkv + cq), bk = *(const f32x4*)(a.bqkv + C + cq);
+          *(uint2*)(Qc + rowc(t, 4 * w + g, 256) + 8 * hh) =
+              uint2{pk_bf16(aq[j][4 * g] + bq[0], aq[j][4 * g + 1] + bq[1]),
+                    pk_bf16(aq[j][4 * g + 2] + bq[2], aq[j][4 * g + 3] + bq[3])};
+          *(uint2*)(Kc + rowc(t, 4 * w + g, 256) + 8 * hh) =
+              uint2{pk_bf16(ak[j][4 * g] + bk[0], ak[j][4 * g + 1] + bk[1]),
+                    pk_bf16(ak[j][4 * g + 2] + bk[2], ak[j][4 * g + 3] + bk[3])};
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int key = 32 * (w >> 1) + rl, qry = 32 * (w & 1) + rl;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const bf16x8 kf = *(const bf16x8*)(Kc + rowc(key, 2 * st + hh, 256));
+        const bf16x8 qf = *(const bf16x8*)(Qc + rowc(qry, 2 * st + hh, 256));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf, sacc, 0, 0, 0);
+      }
+    }
+    __syncthreads();  // Q_c / K_c are rewritten by the next chunk
+  }
+  // ---- 3. softmax over keys: S[query][key] fp32 through LDS, P [query][key] bf16
+  float* const Sm = (float*)(sm + R_QK);              // [64][64 + 4]
+  char* const Pm = sm + R_QK + S * (S + 4) * 4;       // [64][64] bf16, 128-B rows
+  {
+    const int qry = 32 * (w & 1) + rl;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Sm[qry * (S + 4) + 32 * (w >> 1) + 8 * g + 4 * hh + e] = sacc[4 * g + e] * a.scale;
+  }
+  __syncthreads();
+  {
+    const int qry = tid >> 2, k0 = (tid & 3) * 16;
+    float v[16], m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      v[e] = Sm[qry * (S + 4) + k0 + e];
+      m = fmaxf(m, v[e]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    m = fmaxf(m, __shfl_xor(m, 2, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      v[e] = expf(v[e] - m);
+      sum += v[e];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc)
+      *(u32x4*)(Pm + row64(qry, 2 * (tid & 3) + hc)) =
+          u32x4{pk_bf16(v[8 * hc] * inv, v[8 * hc + 1] * inv), pk_bf16(v[8 * hc + 2] * inv, v[8 * hc + 3] * inv),
+                pk_bf16(v[8 * hc + 4] * inv, v[8 * hc + 5] * inv), pk_bf16(v[8 * hc + 6] * inv, v[8 * hc + 7] * inv)};
+  }
+  __syncthreads();
+  // ---- 4. O^T = V^T P^T: D[c][query], wave w: channel blocks CBW w .. x 2 query blocks -> O [token][C] (hn's space)
+  {
+    f32x16 acc[CBW][2];
+#pragma unroll
+    for (int b = 0; b < CBW; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const bf16x8 p0 = *(const bf16x8*)(Pm + row64(rl, 2 * st + hh));
+      const bf16x8 p1 = *(const bf16x8*)(Pm + row64(32 + rl, 2 * st + hh));
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) {
+        const int c = 32 * (CBW * w + b) + rl;
+        const bf16x8 vf = *(const bf16x8*)(sm + R_VT + row64(c, 2 * st + hh));
+        acc[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p0, acc[b][0], 0, 0, 0);
+        acc[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p1, acc[b][1], 0, 0, 0);
+      }
+    }
+    // hn is dead since phase 2: O goes to its rows. lane: query 32 j + rl, channels 32 cb + 8 g + 4 hh + e
+#pragma unroll
+    for (int b = 0; b < CBW; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(uint2*)(sm + rowc(32 * j + rl, 4 * (CBW * w + b) + g, C * 2) + 8 * hh) =
+              uint2{pk_bf16(acc[b][j][4 * g], acc[b][j][4 * g + 1]), pk_bf16(acc[b][j][4 * g + 2], acc[b][j][4 * g + 3])};
+  }
+  __syncthreads();
+  // ---- 5. out = x + O Wp^T + bp: D[c'][token], wave w: blocks CBW w .. x 2 token blocks
+  {
+    f32x16 acc[CBW][2];
+#pragma unroll
+    for (int b = 0; b < CBW; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
+    constexpr int PF = 4;
+    bf16x8 aw[PF][CBW];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) aw[p][b] = *frag(a.wp, CBW * w + b, p);
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      bf16x8 cur[CBW];
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) cur[b] = aw[st % PF][b];
+      if (st + PF < KS)
+#pragma unroll
+        for (int b = 0; b < CBW; ++b) aw[st % PF][b] = *frag(a.wp, CBW * w + b, st + PF);
+      const bf16x8 o0 = hn_frag(rl, st), o1 = hn_frag(32 + rl, st);
+#pragma unroll
+      for (int b = 0; b < CBW; ++b) {
+        acc[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[b][0], 0, 0, 0);
+        acc[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o1, acc[b][1], 0, 0, 0);
+      }
+    }
+    bf16_t* out = a.out + (size_t)img * S * C;
+#pragma unroll
+    for (int b = 0; b < CBW; ++b) {
+      const int cb = CBW * w + b;
+      float s16[16], q16[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = 32 * j + rl;
+        uint32_t wv[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * cb + 8 * g + 4 * hh;
+          const f32x4 bb = *(const f32x4*)(a.bp + c);
+          const uint2 rr = *(const uint2*)(x + (size_t)t * C + c);
+          const float v0 = acc[b][j][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
+          const float v1 = acc[b][j][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
+          const float v2 = acc[b][j][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
+          const float v3 = acc[b][j][4 * g + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
+          wv[g][0] = pk_bf16(v0, v1);
+          wv[g][1] = pk_bf16(v2, v3);
+          const float r0 = __uint_as_float(wv[g][0] << 16), r1 = __uint_as_float(wv[g][0] & 0xffff0000u);
+          const float r2 = __uint_as_float(wv[g][1] << 16), r3 = __uint_as_float(wv[g][1] & 0xffff0000u);
+          s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
+          s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
+          s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
+          s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
+        }
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+          u32x4 o;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+            o[d] = sw[0];
+            o[2 + d] = sw[1];
+          }
+          *(u32x4*)(out + (size_t)t * C + 32 * cb + 8 * (gp + hh)) = o;
+        }
+      }
+      if (a.out_stats) {  // one 64-token slot per image: butterfly over the 32 token lanes
+        float v[32];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          v[e] = s16[e];
+          v[16 + e] = q16[e];
+        }
+        auto xchg = [](float xv, auto wc) {
+          constexpr int wd = decltype(wc)::value;
+          const int xi = __builtin_bit_cast(int, xv);
+          int r;
+          if constexpr (wd == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+          else if constexpr (wd == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+          else if constexpr (wd == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+          else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (wd << 10));
+          return __builtin_bit_cast(float, r);
+        };
+        auto halve = [&](auto wc) {
+          constexpr int wd = decltype(wc)::value;
+          const bool up = (rl & wd) != 0;
+#pragma unroll
+          for (int ii = 0; ii < wd; ++ii) {
+            const float lo = v[ii], hi = v[ii + wd];
+            v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+          }
+        };
+        halve(std::integral_constant<int, 16>{});
+        halve(std::integral_constant<int, 8>{});
+        halve(std::integral_constant<int, 4>{});
+        halve(std::integral_constant<int, 2>{});
+        halve(std::integral_constant<int, 1>{});
+        const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
+        a.out_stats[((long long)img * 2 + (rl >> 4)) * C + co] = v[0];
+      }
+    }
+  }
+}
+
+hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
+  if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(256), 0, s, a);
+  else if (C == 256) ITSD_LAUNCH(attn_block_kernel<256>, dim3(a.n), dim3(256), 0, s, a);
+  else if (C == 128) ITSD_LAUNCH(attn_block_kernel<128>, dim3(a.n), dim3(256), 0, s, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+bool attn_block_ok(int S, int C) { return S == 64 && (C == 128 || C == 256 || C == 384); }  // LDS: C <= 384
 
 // Flash-style MFMA attention for long sequences (S > 256: the CFG UNet's 32x32 level,
 // S = 1024, C = 128, ModelCondition.py:98-118; Arch A at 64/256 px). No S x S tile is

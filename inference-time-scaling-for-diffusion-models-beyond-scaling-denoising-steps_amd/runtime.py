@@ -211,7 +211,8 @@ class NativeUNet:
                                      kinds.ctypes.data, ms.ctypes.data, fl.ctypes.data, sh.ctypes.data,
                                      ctypes.byref(n), stream_ptr(x.device)))
         k = n.value
-        names = {0: "gn", 1: "conv", 2: "attn", 3: "gncoef", 4: "convgn", 5: "convgnw", 6: "convgnw4", -1: "head", -2: "tail"}
+        names = {0: "gn", 1: "conv", 2: "attn", 3: "gncoef", 4: "convgn", 5: "convgnw", 6: "convgnw4", 7: "attnblock",
+                 -1: "head", -2: "tail"}
         L = lib()
 
         def decode(v: int):  # (kernel id << 8) | op class as a signed byte
