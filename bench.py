@@ -51,6 +51,7 @@ KERNEL_NAMES = {  # op classes of the census
     "convgnw4": "fused GroupNorm+SiLU+conv3x3, 256-pixel tiles of four 8x8 images",
     "conv": "implicit-GEMM conv (1x1, strided, sub-pixel upsample, 4x4 level)",
     "attn": "self-attention on MFMA",
+    "attnblock": "fused AttnBlock (GroupNorm + q|k|v + attention + proj)",
 }
 
 
@@ -216,7 +217,7 @@ def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
     n_l, ms_census, fl_sum, idx, kind, inst = per[func]
     # each launch replayed 10x back to back between HIP events (itsd_profile_op): what the
     # replayed step graph sees, without the eager census's per-launch event overhead
-    ms_of = {i: (nat.profile_op(x, t, i, reps=10) if steady else ops[i]["ms"]) for i in idx}
+    ms_of = {i: (nat.profile_op(x, t, ops[i]["op"], reps=10) if steady else ops[i]["ms"]) for i in idx}
     ms_sum = sum(ms_of.values())
     achieved = fl_sum / (ms_sum * 1e-3) / 1e12
     peak = MFMA_BF16_PEAK_TFLOPS if precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
@@ -439,14 +440,23 @@ def main():
                          "pmc_frac_of_peak": round(traffic / avg_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
                          "peak_gbps": HBM_PEAK_GBPS},
         })
-        if "attn" in agg:
-            al, ams, afl = agg["attn"]
-            at = afl / (ams * 1e-3) / 1e12
-            akern = sorted({rocprof_name(o["kernel"]) for o in ops if o["kind"] == "attn"})
-            roof["attention"] = {"kernel": " / ".join(akern), "launches_per_forward": al,
-                                 "avg_launch_ms": round(ams / al, 4), "tflops": round(at, 2),
-                                 "mfma_frac": round(at / MFMA_BF16_PEAK_TFLOPS, 4),
-                                 "share_of_forward": round(ams / total_ms, 4)}
+        # attention (north_star: MFMA utilisation): the fused AttnBlock kernel (GroupNorm, q|k|v and
+        # proj projections, softmax attention in one launch; its FLOPs are all of those) and the
+        # plain attention kernel where an AttnBlock is not fused (the 4x4 level)
+        att = {}
+        for kind in ("attnblock", "attn"):
+            if kind in agg:
+                al, ams, afl = agg[kind]
+                at = afl / (ams * 1e-3) / 1e12
+                akern = sorted({rocprof_name(o["kernel"]) for o in ops if o["kind"] == kind})
+                att[kind] = {"kernel": " / ".join(akern), "launches_per_forward": al,
+                             "avg_launch_ms": round(ams / al, 4), "tflops": round(at, 2),
+                             "mfma_frac": round(at / MFMA_BF16_PEAK_TFLOPS, 4),
+                             "share_of_forward": round(ams / total_ms, 4)}
+        if att:
+            roof["attention"] = att.get("attnblock", att.get("attn"))
+            if len(att) > 1:
+                roof["attention"]["unfused"] = att["attn"]
 
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:

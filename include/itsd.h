@@ -148,8 +148,11 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
  * (head, program ops in order, tail GN, tail) kinds[i] = (kernel << 8) | (kind & 0xff) with
  * kind the op class (0 GN, 1 conv, 2 attention, 3 GN finalize, 4/5/6 fused GroupNorm conv
  * 128 px / 256 px / 8x8 level; -1 head, -2 tail, as a signed byte) and kernel the id of
- * the first kernel the launch ran (itsd_kernel_name), ms[i], flops[i] and shapes[6*i..] =
- * {M, Cout, K or Cin, Hout, ksize, 10*stride+upsample}. CFG UNets run with label 0.
+ * the first kernel the launch ran (itsd_kernel_name), ms[i], flops[i] and shapes[8*i..] =
+ * {M, Cout, K or Cin, Hout, ksize, 10*stride+upsample, op, 0} with op the program op index
+ * (1-based, itsd_profile_op's numbering; 0 = head / tail). Ops whose launch is folded into the
+ * next one (a GroupNorm finalize done by conv3x3_gn_p5_kernel) have no entry. kind 7 = the fused
+ * AttnBlock. CFG UNets run with label 0.
  * At most max_ops entries; *n_ops = entries written. */
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
                      double* ms, double* flops, int* shapes, int* n_ops, void* stream);

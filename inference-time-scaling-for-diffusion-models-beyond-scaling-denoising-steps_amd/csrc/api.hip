@@ -42,6 +42,7 @@ hipError_t launch_run_begin(int*, int, int*, RunParams*, const RunParams&, hipSt
 int g_option_gen = 0;  // bumped by every itsd_set_option: part of the step-graph cache key
 bool conv_gn_eligible(int H, int W);
 bool p5_eligible(int H, int W);
+bool conv_p5_selected(const ConvArgs& a);
 int conv_gn_wide_segs(int H, int W, int M, int Cout);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
@@ -117,6 +118,7 @@ struct Op {
   int vt = -1, vt_from = 0;  // channel-major V buffer (conv: couts >= vt_from go there; attn: reads it)
   size_t coef = SIZE_MAX;    // GNCOEF: output; CONV: GroupNorm+SiLU coefficients of the input (fused conv)
   size_t wt2 = 0, bias2 = 0;  // ATTNBLOCK: the proj matrix (fragment-packed) and bias; wt / bias: q|k|v
+  size_t gn_gamma = SIZE_MAX, gn_beta = SIZE_MAX;  // CONV with coef: its input GroupNorm's affine (gn_fold)
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -400,6 +402,10 @@ struct Builder {
     int dst = act(Hout, Wout, Cout);
     conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
     u->ops.back().coef = coef;
+    if (coef != SIZE_MAX) {  // (the GNCOEF op pushed just before this conv)
+      u->ops.back().gn_gamma = u->ops[u->ops.size() - 2].gamma;
+      u->ops.back().gn_beta = u->ops[u->ops.size() - 2].beta;
+    }
     if (coef != SIZE_MAX && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
       u->ops.back().wfrag = pack_frag(W, Cout, Cin, ks);
     if (coef != SIZE_MAX && u->bf16 && Cout % 16 == 0 && (ks * ks * Cin) % 32 == 0 && ks == 3 && Hout >= 16)
@@ -706,42 +712,11 @@ struct RunCtx {
   std::vector<int>* ev_kind = nullptr;
   std::vector<double>* ev_flops = nullptr;
   std::vector<int>* ev_kid = nullptr;  // kernel_id of the op's first launch (itsd_kernel_name)
+  std::vector<int>* ev_op = nullptr;   // program op index (1-based; 0 = head / tail) of each launch
 };
 
-int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
-  hipError_t e = hipSuccess;
-  if (o.kind == OP_GNCOEF) {
-    GNArgs g{};
-    g.C1 = u->acts[o.src1].C;
-    g.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
-    g.HW = u->acts[o.src1].H * u->acts[o.src1].W;
-    g.gamma = u->wp(o.gamma);
-    g.beta = u->wp(o.beta);
-    g.eps = 1e-5f;
-    g.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
-    g.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
-    g.spi1 = u->acts[o.src1].spi;
-    g.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
-    e = launch_gn_coef(g, c.nb, (float*)(u->ws + o.coef), s);
-  } else if (o.kind == OP_GN) {
-    GNArgs a{};
-    a.src1 = u->ap(o.src1);
-    a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
-    a.C1 = u->acts[o.src1].C;
-    a.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
-    a.HW = u->acts[o.src1].H * u->acts[o.src1].W;
-    a.gamma = u->wp(o.gamma);
-    a.beta = u->wp(o.beta);
-    a.eps = 1e-5f;
-    a.silu = o.silu;
-    a.dst = u->ap(o.dst);
-    a.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
-    a.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
-    a.spi1 = u->acts[o.src1].spi;
-    a.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
-    e = u->bf16 ? launch_groupnorm<bf16_t>(a, c.nb, s) : launch_groupnorm<float>(a, c.nb, s);
-  } else if (o.kind == OP_CONV) {
-    ConvArgs a{};
+// The launch arguments of a conv op (shared by launch_op and run_program's gn_fold decision).
+int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     const Act& in = u->acts[o.src1];
     const Act& out = u->acts[o.dst];
     a.src1 = u->ap(o.src1);
@@ -801,6 +776,55 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
       if (a.C1 % epc || a.C2 % epc || a.Cout % 4 || a.K % epc)
         return fail(ITSD_ERR_INVALID, "conv channels must be multiples of " + std::to_string(epc));
     }
+  // gn_fold: conv3x3_gn_p5_kernel reduces the input's statistics slabs itself (run_program then
+  // skips the op's gn_coef launch)
+  if (a.gn_coef && o.gn_gamma != SIZE_MAX && itsd::g_gn_fold && (a.C1 + a.C2) % 128 == 0 && conv_p5_selected(a)) {
+    a.gn_fold = 1;
+    a.gn_st1 = (const float*)(u->ws + u->acts[o.src1].stats);
+    a.gn_st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    a.gn_spi1 = u->acts[o.src1].spi;
+    a.gn_spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
+    a.gn_gamma = u->wp(o.gn_gamma);
+    a.gn_beta = u->wp(o.gn_beta);
+  }
+  return ITSD_OK;
+}
+
+int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (o.kind == OP_GNCOEF) {
+    GNArgs g{};
+    g.C1 = u->acts[o.src1].C;
+    g.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
+    g.HW = u->acts[o.src1].H * u->acts[o.src1].W;
+    g.gamma = u->wp(o.gamma);
+    g.beta = u->wp(o.beta);
+    g.eps = 1e-5f;
+    g.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
+    g.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    g.spi1 = u->acts[o.src1].spi;
+    g.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
+    e = launch_gn_coef(g, c.nb, (float*)(u->ws + o.coef), s);
+  } else if (o.kind == OP_GN) {
+    GNArgs a{};
+    a.src1 = u->ap(o.src1);
+    a.src2 = o.src2 >= 0 ? u->ap(o.src2) : nullptr;
+    a.C1 = u->acts[o.src1].C;
+    a.C2 = o.src2 >= 0 ? u->acts[o.src2].C : 0;
+    a.HW = u->acts[o.src1].H * u->acts[o.src1].W;
+    a.gamma = u->wp(o.gamma);
+    a.beta = u->wp(o.beta);
+    a.eps = 1e-5f;
+    a.silu = o.silu;
+    a.dst = u->ap(o.dst);
+    a.st1 = (const float*)(u->ws + u->acts[o.src1].stats);
+    a.st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;
+    a.spi1 = u->acts[o.src1].spi;
+    a.spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
+    e = u->bf16 ? launch_groupnorm<bf16_t>(a, c.nb, s) : launch_groupnorm<float>(a, c.nb, s);
+  } else if (o.kind == OP_CONV) {
+    ConvArgs a{};
+    CHK(conv_args(u, o, c, a));
     e = u->bf16 ? launch_conv<bf16_t>(a, s) : launch_conv<float>(a, s);
   } else if (o.kind == OP_ATTNBLOCK) {
     AttnBlockArgs a{};
@@ -845,8 +869,10 @@ double op_flops(const itsd_unet* u, const Op& o, int nb) {
 }
 
 int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
+  int cur_op = 0;  // program op being launched (census: 1-based, 0 head / tail)
   auto mark = [&](int kind, double fl, const std::function<int()>& fn) -> int {
     if (!c.census) return fn();
+    if (c.ev_op) c.ev_op->push_back(cur_op);
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
@@ -880,8 +906,14 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     return e == hipSuccess ? ITSD_OK : fail(ITSD_ERR_HIP, hipGetErrorString(e));
   }));
   // census kinds: OpKind, and kCensusConvGN for the fused GroupNorm+SiLU convs
-  for (const Op& o : u->ops) {
+  for (size_t oi = 0; oi < u->ops.size(); ++oi) {
+    const Op& o = u->ops[oi];
+    if (o.kind == OP_GNCOEF && oi + 1 < u->ops.size() && u->ops[oi + 1].kind == OP_CONV) {
+      ConvArgs na{};  // gn_fold: the consumer conv finalizes this GroupNorm itself
+      if (conv_args(u, u->ops[oi + 1], c, na) == ITSD_OK && na.gn_fold) continue;
+    }
     int kind = o.kind == OP_ATTNBLOCK ? kCensusAttnBlock : (int)o.kind;
+    cur_op = (int)oi + 1;
     if (o.kind == OP_CONV && o.coef != SIZE_MAX) {
       const Act& out = u->acts[o.dst];
       const int segs = u->bf16 ? conv_gn_wide_segs(out.H, out.W, c.nb * out.H * out.W, o.Cout) : 0;
@@ -890,6 +922,7 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     CHK(mark(kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
   }
   // tail GN + conv (+ sampler update); bf16 MFMA tail: GN coefficients, then one fused launch
+  cur_op = 0;
   Op g;
   g.src1 = u->tail_in; g.gamma = u->tail_gn_g; g.beta = u->tail_gn_b; g.silu = 1;
   if (u->tail_wmf != SIZE_MAX) {
@@ -1092,6 +1125,10 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p5_split")) {  // its K slices: 0 auto (cost model), 1..16 forced
     if (value < 0 || value > 16) return fail(ITSD_ERR_INVALID, "p5_split in [0,16]");
     itsd::g_p5_split = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p5_kernel: 0 off, 1 on
+    itsd::g_gn_fold = value ? 1 : 0;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards
@@ -1455,14 +1492,14 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
   }
   CHK(temb_rows(u, t, n, 0, false, u->proj_buf, s));
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
-  std::vector<int> kd, kid;
+  std::vector<int> kd, kid, eop;
   std::vector<double> fl;
   RunCtx c{};
   c.nb = n; c.x = x; c.x_mod = n;
   c.temb = u->proj_buf; c.temb_img_stride = u->sumC;
   c.labels = lab0; c.label_mod = n; c.uncond_from = -1;
   c.tail.n = n; c.tail.step_mode = 0; c.tail.eps_out = eps;
-  c.census = true; c.evs = &evs; c.ev_kind = &kd; c.ev_flops = &fl; c.ev_kid = &kid;
+  c.census = true; c.evs = &evs; c.ev_kind = &kd; c.ev_flops = &fl; c.ev_kid = &kid; c.ev_op = &eop;
   int r = run_program(u, c, s);
   hipError_t e = hipStreamSynchronize(s);
   // launch order: head, ops..., tail GN, tail
@@ -1477,10 +1514,11 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
     if (ms) ms[k] = m;
     if (flops) flops[k] = fl[i];
     if (shapes) {
-      int* sh = shapes + 6 * k;
-      for (int q = 0; q < 6; ++q) sh[q] = 0;
-      if (i >= 1 && i - 1 < u->ops.size()) {
-        const Op& o = u->ops[i - 1];
+      int* sh = shapes + 8 * k;
+      for (int q = 0; q < 8; ++q) sh[q] = 0;
+      sh[6] = eop[i];
+      if (eop[i] >= 1) {
+        const Op& o = u->ops[eop[i] - 1];
         const Act& out = u->acts[o.dst >= 0 ? o.dst : o.src1];
         const Act& in = u->acts[o.src1];
         sh[0] = n * out.H * out.W;

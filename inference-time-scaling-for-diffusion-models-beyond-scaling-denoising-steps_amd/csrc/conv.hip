@@ -54,6 +54,7 @@ int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
+int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
 int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
                          // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
 
@@ -1891,8 +1892,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   constexpr int ITEMS = Cf::ITEMS, HALO = Cf::HALO, TH = Cf::TH, HY0 = Cf::HY0, NHY = Cf::NHY;
   constexpr int SPX = TH * W;  // pixels of one segment
   static_assert(NSEG * SPX == 128 && ITEMS * RPP == NHY * W && ITEMS <= 31 && 36 % P5_RING == 0, "p5 geometry");
-  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + 2 * NSEG * CONV_BM * 4];
+  constexpr int SEGW = 64 / TPS > 0 ? 64 / TPS : 1;  // image segments one halo wave covers (W = 4: 2)
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + 2 * NSEG * CONV_BM * 4 + 4 * 2 * SEGW * 64 * 4];
   float* const addv = (float*)(smem + 2 * HALO);  // [item parity][image of the tile][128 couts]
+  // gn_fold: per halo wave, [item parity][segment of the wave][32 groups][mean, rstd]
+  float* const gsw_all = (float*)(smem + 2 * HALO + 2 * NSEG * CONV_BM * 4);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
@@ -2181,6 +2185,60 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   int kL = 0, ccL = 0, c1L = 0;  // the stage being loaded and its item's chunk end
   int pix0 = 0;                  // global pixel of this thread's item 0 of the loaded stage (r = lt >> 3)
   const float* cbase = a.gn_coef;
+  const int hw = (tid >> 6) - 4, sw0 = (64 * hw) / TPS, sl = sg - sw0;  // this wave's first segment; mine in it
+  float* const gsw = gsw_all + hw * 2 * SEGW * 64;
+  // gn_fold: group mean / rstd (fp64 sums of the producers' slabs, as gn_coef_kernel) of the images of
+  // item k that this wave stages -> gsw[k & 1]. Lane = (group lane & 31, half lane >> 5): half a
+  // group's channels, 2 at a time, every load of a slot issued before any is used (unconditional
+  // loads from clamped addresses, then a select: no branch / wait per element)
+  auto group_stats = [&](int k) {
+    int tp, tc, z;
+    item_of(k, tp, tc, z);
+    const int g = lane & 31, hf = Cin / 64, c0 = g * 2 * hf + (lane >> 5) * hf;  // (Cin / 32 channels a group)
+    const int sp1 = stat_spi(HW, a.gn_spi1), sp2 = a.C2 ? stat_spi(HW, a.gn_spi2) : 0;
+    const int spm = sp1 > sp2 ? sp1 : sp2;
+#pragma unroll
+    for (int segl = 0; segl < SEGW; ++segl) {
+      const int img = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sw0 + segl;
+      const int imgc = img < nimg ? img : nimg - 1;
+      double sm = 0.0, sq = 0.0;
+      for (int q = 0; q < spm; ++q)
+      for (int cb0 = 0; cb0 < hf; cb0 += 16) {  // passes of 16 channels of the half group (hf = Cin / 64, even)
+        float2 vs[8], vq[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int cr = c0 + cb0 + 2 * i;
+          const bool s1 = cr < a.C1;
+          const int spi = s1 ? sp1 : sp2;
+          const bool ok = cb0 + 2 * i < hf && q < spi;
+          const int c = ok ? cr : c0, qq = ok ? q : 0;
+          const bool t1 = c < a.C1;
+          const float* st = t1 ? a.gn_st1 : a.gn_st2;
+          const int Cs = t1 ? a.C1 : a.C2, cs = t1 ? c : c - a.C1, sp = t1 ? sp1 : sp2;
+          const long long slot = (long long)imgc * sp + qq;
+          const float2 u0 = *(const float2*)(st + (slot * 2) * Cs + cs);
+          const float2 u1 = *(const float2*)(st + (slot * 2 + 1) * Cs + cs);
+          vs[i] = ok ? u0 : float2{0.f, 0.f};
+          vq[i] = ok ? u1 : float2{0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          sm += (double)vs[i].x + (double)vs[i].y;
+          sq += (double)vq[i].x + (double)vq[i].y;
+        }
+      }
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      const double E = (double)(Cin / 32) * HW, mean = sm / E;
+      double var = sq / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      if (lane < 32) {
+        float* d = gsw + ((k & 1) * SEGW + segl) * 64 + 2 * g;
+        d[0] = (float)mean;
+        d[1] = (float)(1.0 / sqrt(var + 1e-5));
+      }
+    }
+  };
   auto open_item = [&](int k) __attribute__((always_inline)) {  // geometry of item k (as the loaded stage)
     int tp, tc, z;
     item_of(k, tp, tc, z);
@@ -2197,17 +2255,41 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       zmn |= (uint32_t)(img < nimg && y >= 0 && y < W) << j;  // (square images: H = W)
     }
     cbase = a.gn_coef + ((size_t)imgc * (Cin / 8) + lch) * 16;
+    if (a.gn_fold) group_stats(k);
   };
-  auto load_stage = [&]() __attribute__((always_inline)) {  // coefficients + items of stage L
-    const f32x4* cp = (const f32x4*)(cbase + ccL * 128);
+  // stage L's GroupNorm+SiLU coefficients of this lane's 8 channels (gn_fold: gamma / beta, turned
+  // into a, b by prescale from the wave's group statistics)
+  auto load_stage = [&]() __attribute__((always_inline)) {
+    if (a.gn_fold) {
+      const int c0 = ccL * 64 + 8 * lch;
+      cn[0] = *(const f32x4*)(a.gn_gamma + c0);
+      cn[1] = *(const f32x4*)(a.gn_gamma + c0 + 4);
+      cn[2] = *(const f32x4*)(a.gn_beta + c0);
+      cn[3] = *(const f32x4*)(a.gn_beta + c0 + 4);
+    } else {
+      const f32x4* cp = (const f32x4*)(cbase + ccL * 128);
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) cn[qq] = cp[qq];
+      for (int qq = 0; qq < 4; ++qq) cn[qq] = cp[qq];
+    }
   };
   auto prescale = [&]() __attribute__((always_inline)) {
+    if (a.gn_fold) {  // a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula), per channel's group
+      const int c0 = ccL * 64 + 8 * lch, gsz = Cin / 32;
+      const float* gs = gsw + ((kL & 1) * SEGW + sl) * 64;
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
+      for (int e = 0; e < 8; ++e) {
+        const int g = (c0 + e) / gsz;
+        const float mean = gs[2 * g], rstd = gs[2 * g + 1];
+        const float sc = rstd * cn[e >> 2][e & 3];
+        c[e >> 2][e & 3] = sc * GN_L2E;
+        c[2 + (e >> 2)][e & 3] = (cn[2 + (e >> 2)][e & 3] - mean * sc) * GN_L2E;
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) c[qq][e] = cn[qq][e] * GN_L2E;
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c[qq][e] = cn[qq][e] * GN_L2E;
+    }
     zm = zmn;
   };
   bool more = true;  // a stage L exists
@@ -2512,14 +2594,22 @@ static int p5_split(const ConvArgs& a, int tiles, int nch) {
     S = std::min(g_p5_split, nch);
   } else {
     double best = 1e30;
+    // (the last arriving slice of a tile reads all S partials: ~0.3 chunk-times a slice)
     for (int s = 1; s <= std::min(nch, 16); ++s) {
       const double waves = std::ceil((double)tiles * s / g_num_cus);
-      const double cost = waves * (std::ceil((double)nch / s) + 1.5);
+      const double cost = waves * (std::ceil((double)nch / s) + 1.5) + (s > 1 ? 0.3 * s : 0.0);
       if (cost < best - 1e-9) { best = cost; S = s; }
     }
   }
   while (S > 1 && ((long long)tiles * S * 4 * 4096 > a.splitk_cap || (long long)tiles * 4 > kTicketCap)) --S;
   return S;
+}
+
+// launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p5_kernel?
+bool conv_p5_selected(const ConvArgs& a) {
+  if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
+  const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
+  return a.Wout == 4 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
 }
 
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
@@ -2588,11 +2678,8 @@ template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (a.gn_coef) {
-      if (a.wfrag && a.Cout % CONV_BM == 0 && a.C1 % 64 == 0 && a.C2 % 64 == 0 && p5_eligible(a.Hout, a.Wout)) {
-        // the 4x4 level always (no other fused kernel holds it); the others where p4 under-fills the chip
-        const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
-        if (a.Wout == 4 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192)) return launch_p5(a, s);
-      }
+      // the 4x4 level always (no other fused kernel holds it); the others where p4 under-fills the chip
+      if (conv_p5_selected(a)) return launch_p5(a, s);
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
         const bool p4 = g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
                         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));

@@ -333,13 +333,14 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
 // 4-k-step prefetch; one block per image.
 
 template <int C>
-__global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
-  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128;
+__global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
   static_assert(C % 128 == 0, "C");
-  constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256;
-  __shared__ __attribute__((aligned(16))) char sm[R_GS + 32 * 2 * 4];
+  constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256, R_ST = R_GS + 32 * 2 * 4;
+  __shared__ __attribute__((aligned(16))) char sm[R_ST + 2 * C * 2 * 4];
   const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = w & 3, wt = w >> 2;  // wave = (channel-block group, token block)
   const int img = blockIdx.x;
   const bf16_t* x = a.x + (size_t)img * S * C;
   // [row][C] bf16 image, 16-B chunk ch of row r at (ch ^ (r & 15))
@@ -349,9 +350,16 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
   auto frag = [&](const bf16_t* W, int cb, int st) -> const bf16x8* {
     return (const bf16x8*)((const char*)W + ((size_t)cb * KS + st) * 1024 + lane * 16);
   };
-  // ---- 0. GroupNorm statistics -> (mean, rstd) per group; hn
+  // ---- 0. GroupNorm statistics -> (mean, rstd) per group; hn (all x loads issued before any use)
+  constexpr int XU = S * (C / 8) / 512;  // 16-B units of x per thread
+  u32x4 xv[XU];
+#pragma unroll
+  for (int i = 0; i < XU; ++i) {
+    const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8);
+    xv[i] = *(const u32x4*)(x + (size_t)t * C + ch * 8);
+  }
   float* gs = (float*)(sm + R_GS);
-  {
+  if (tid < 256) {
     const int g = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
     double s = 0.0, q = 0.0;
     for (int k = l8; k < n_it; k += 8) {
@@ -374,9 +382,9 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
     }
   }
   __syncthreads();
-  for (int u = tid; u < S * (C / 8); u += 256) {
-    const int t = u / (C / 8), ch = u - t * (C / 8), c0 = ch * 8;
-    const u32x4 v = *(const u32x4*)(x + (size_t)t * C + c0);
+#pragma unroll
+  for (int i = 0; i < XU; ++i) {
+    const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8), c0 = ch * 8;
     uint32_t o[4];
 #pragma unroll
     for (int e2 = 0; e2 < 4; ++e2) {
@@ -386,8 +394,8 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
         const int c = c0 + 2 * e2 + h2, g = c / (C / 32);  // (an 8-channel chunk may straddle two groups)
         const float mean = gs[2 * g], rstd = gs[2 * g + 1];
         const float sc = rstd * a.gamma[c];
-        const float xv = __uint_as_float(h2 ? (v[e2] & 0xffff0000u) : (v[e2] << 16));
-        y[h2] = xv * sc + (a.beta[c] - mean * sc);
+        const float xf = __uint_as_float(h2 ? (xv[i][e2] & 0xffff0000u) : (xv[i][e2] << 16));
+        y[h2] = xf * sc + (a.beta[c] - mean * sc);
       }
       o[e2] = pk_bf16(y[0], y[1]);
     }
@@ -396,22 +404,20 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
   __syncthreads();
   // hn fragment of (token row r, k-step st): lane (rl, hh) reads channels 16 st + 8 hh ..
   auto hn_frag = [&](int r, int st) { return *(const bf16x8*)(sm + rowc(r, 2 * st + hh, C * 2)); };
+  const int tr = 32 * wt + rl;  // this wave's token / query row
 
-  // ---- 1. V^T: D[token][c] = hn Wv^T; wave w owns channel blocks CBW w .. (x 2 token blocks)
+  // ---- 1. V^T: D[token][c] = hn Wv^T; wave: channel blocks CBW wq .. x token block wt
   {
-    f32x16 acc[2][CBW];
+    f32x16 acc[CBW];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int b = 0; b < CBW; ++b)
 #pragma unroll
-      for (int b = 0; b < CBW; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][b][r] = 0.f;
-    constexpr int PF = 4;
+      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
     bf16x8 bw[PF][CBW];
 #pragma unroll
     for (int p = 0; p < PF; ++p)
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) bw[p][b] = *frag(a.wqkv, 2 * CB + CBW * w + b, p);
+      for (int b = 0; b < CBW; ++b) bw[p][b] = *frag(a.wqkv, 2 * CB + CBW * wq + b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       bf16x8 cur[CBW];
@@ -419,29 +425,23 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
       for (int b = 0; b < CBW; ++b) cur[b] = bw[st % PF][b];
       if (st + PF < KS)
 #pragma unroll
-        for (int b = 0; b < CBW; ++b) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + CBW * w + b, st + PF);
-      const bf16x8 h0 = hn_frag(rl, st), h1 = hn_frag(32 + rl, st);
+        for (int b = 0; b < CBW; ++b) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + CBW * wq + b, st + PF);
+      const bf16x8 h0 = hn_frag(tr, st);
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) {
-        acc[0][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur[b], acc[0][b], 0, 0, 0);
-        acc[1][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h1, cur[b], acc[1][b], 0, 0, 0);
-      }
+      for (int b = 0; b < CBW; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur[b], acc[b], 0, 0, 0);
     }
-    // lane: channel c = 32 cb + rl (column), tokens 32 i + 8 g + 4 hh + e (rows)
+    // lane: channel c = 32 cb + rl (column), tokens 32 wt + 8 g + 4 hh + e (rows)
 #pragma unroll
     for (int b = 0; b < CBW; ++b) {
-      const int c = 32 * (CBW * w + b) + rl;
+      const int c = 32 * (CBW * wq + b) + rl;
       const float bv = a.bqkv[2 * C + c];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(uint2*)(sm + R_VT + row64(c, 4 * i + g) + 8 * hh) =
-              uint2{pk_bf16(acc[i][b][4 * g] + bv, acc[i][b][4 * g + 1] + bv),
-                    pk_bf16(acc[i][b][4 * g + 2] + bv, acc[i][b][4 * g + 3] + bv)};
+      for (int g = 0; g < 4; ++g)
+        *(uint2*)(sm + R_VT + row64(c, 4 * wt + g) + 8 * hh) =
+            uint2{pk_bf16(acc[b][4 * g] + bv, acc[b][4 * g + 1] + bv), pk_bf16(acc[b][4 * g + 2] + bv, acc[b][4 * g + 3] + bv)};
     }
   }
-  // ---- 2. Q_c, K_c per 128-channel chunk; S^T (keys x queries) tile (w >> 1, w & 1) in registers
+  // ---- 2. Q_c, K_c per 128-channel chunk; S^T (keys x queries) tile w (waves 0..3) in registers
   f32x16 sacc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
@@ -449,51 +449,40 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
   char* const Kc = sm + R_QK + S * 256;
   for (int ch = 0; ch < NCH; ++ch) {
     {
-      f32x16 aq[2], ak[2];
+      f32x16 aq, ak;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) aq[j][r] = ak[j][r] = 0.f;
-      const int cbq = 4 * ch + w, cbk = CB + 4 * ch + w;
-      constexpr int PF = 4;
-      bf16x8 wq[PF], wk[PF];
+      for (int r = 0; r < 16; ++r) aq[r] = ak[r] = 0.f;
+      const int cbq = 4 * ch + wq, cbk = CB + 4 * ch + wq;
+      bf16x8 fq[PF], fk[PF];
 #pragma unroll
       for (int p = 0; p < PF; ++p) {
-        wq[p] = *frag(a.wqkv, cbq, p);
-        wk[p] = *frag(a.wqkv, cbk, p);
+        fq[p] = *frag(a.wqkv, cbq, p);
+        fk[p] = *frag(a.wqkv, cbk, p);
       }
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
-        const bf16x8 q_ = wq[st % PF], k_ = wk[st % PF];
+        const bf16x8 q_ = fq[st % PF], k_ = fk[st % PF];
         if (st + PF < KS) {
-          wq[st % PF] = *frag(a.wqkv, cbq, st + PF);
-          wk[st % PF] = *frag(a.wqkv, cbk, st + PF);
+          fq[st % PF] = *frag(a.wqkv, cbq, st + PF);
+          fk[st % PF] = *frag(a.wqkv, cbk, st + PF);
         }
-        const bf16x8 h0 = hn_frag(rl, st), h1 = hn_frag(32 + rl, st);
-        aq[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h0, aq[0], 0, 0, 0);
-        aq[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h1, aq[1], 0, 0, 0);
-        ak[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h0, ak[0], 0, 0, 0);
-        ak[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h1, ak[1], 0, 0, 0);
+        const bf16x8 h0 = hn_frag(tr, st);
+        aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h0, aq, 0, 0, 0);
+        ak = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h0, ak, 0, 0, 0);
       }
-      // lane: token 32 j + rl (column), channels 32 w + 8 g + 4 hh + e of the chunk (rows)
+      // lane: token tr (column), channels 32 wq + 8 g + 4 hh + e of the chunk (rows)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int t = 32 * j + rl;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int cq = 128 * ch + 32 * w + 8 * g + 4 * hh;
-          const f32x4 bq = *(const f32x4*)(a.bqkv + cq), bk = *(const f32x4*)(a.bqkv + C + cq);
-          *(uint2*)(Qc + rowc(t, 4 * w + g, 256) + 8 * hh) =
-              uint2{pk_bf16(aq[j][4 * g] + bq[0], aq[j][4 * g + 1] + bq[1]),
-                    pk_bf16(aq[j][4 * g + 2] + bq[2], aq[j][4 * g + 3] + bq[3])};
-          *(uint2*)(Kc + rowc(t, 4 * w + g, 256) + 8 * hh) =
-              uint2{pk_bf16(ak[j][4 * g] + bk[0], ak[j][4 * g + 1] + bk[1]),
-                    pk_bf16(ak[j][4 * g + 2] + bk[2], ak[j][4 * g + 3] + bk[3])};
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int cq = 128 * ch + 32 * wq + 8 * g + 4 * hh;
+        const f32x4 bq = *(const f32x4*)(a.bqkv + cq), bk = *(const f32x4*)(a.bqkv + C + cq);
+        *(uint2*)(Qc + rowc(tr, 4 * wq + g, 256) + 8 * hh) =
+            uint2{pk_bf16(aq[4 * g] + bq[0], aq[4 * g + 1] + bq[1]), pk_bf16(aq[4 * g + 2] + bq[2], aq[4 * g + 3] + bq[3])};
+        *(uint2*)(Kc + rowc(tr, 4 * wq + g, 256) + 8 * hh) =
+            uint2{pk_bf16(ak[4 * g] + bk[0], ak[4 * g + 1] + bk[1]), pk_bf16(ak[4 * g + 2] + bk[2], ak[4 * g + 3] + bk[3])};
       }
     }
     __syncthreads();
-    {
+    if (w < 4) {
       const int key = 32 * (w >> 1) + rl, qry = 32 * (w & 1) + rl;
 #pragma unroll
       for (int st = 0; st < 8; ++st) {
@@ -507,7 +496,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
   // ---- 3. softmax over keys: S[query][key] fp32 through LDS, P [query][key] bf16
   float* const Sm = (float*)(sm + R_QK);              // [64][64 + 4]
   char* const Pm = sm + R_QK + S * (S + 4) * 4;       // [64][64] bf16, 128-B rows
-  {
+  if (w < 4) {
     const int qry = 32 * (w & 1) + rl;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -516,78 +505,68 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
   }
   __syncthreads();
   {
-    const int qry = tid >> 2, k0 = (tid & 3) * 16;
-    float v[16], m = -INFINITY;
+    const int qry = tid >> 3, k0 = (tid & 7) * 8;  // 8 lanes a query, 8 keys a lane
+    float v[8], m = -INFINITY;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
+    for (int e = 0; e < 8; ++e) {
       v[e] = Sm[qry * (S + 4) + k0 + e];
       m = fmaxf(m, v[e]);
     }
-    m = fmaxf(m, __shfl_xor(m, 1, 64));
-    m = fmaxf(m, __shfl_xor(m, 2, 64));
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     float sum = 0.f;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
+    for (int e = 0; e < 8; ++e) {
       v[e] = expf(v[e] - m);
       sum += v[e];
     }
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    const float inv = 1.0f / sum;
 #pragma unroll
-    for (int hc = 0; hc < 2; ++hc)
-      *(u32x4*)(Pm + row64(qry, 2 * (tid & 3) + hc)) =
-          u32x4{pk_bf16(v[8 * hc] * inv, v[8 * hc + 1] * inv), pk_bf16(v[8 * hc + 2] * inv, v[8 * hc + 3] * inv),
-                pk_bf16(v[8 * hc + 4] * inv, v[8 * hc + 5] * inv), pk_bf16(v[8 * hc + 6] * inv, v[8 * hc + 7] * inv)};
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    const float inv = 1.0f / sum;
+    *(u32x4*)(Pm + row64(qry, tid & 7)) =
+        u32x4{pk_bf16(v[0] * inv, v[1] * inv), pk_bf16(v[2] * inv, v[3] * inv), pk_bf16(v[4] * inv, v[5] * inv),
+              pk_bf16(v[6] * inv, v[7] * inv)};
   }
   __syncthreads();
-  // ---- 4. O^T = V^T P^T: D[c][query], wave w: channel blocks CBW w .. x 2 query blocks -> O [token][C] (hn's space)
+  // ---- 4. O^T = V^T P^T: D[c][query], wave: channel blocks CBW wq .. x query block wt -> O [token][C]
   {
-    f32x16 acc[CBW][2];
+    f32x16 acc[CBW];
 #pragma unroll
     for (int b = 0; b < CBW; ++b)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
-      const bf16x8 p0 = *(const bf16x8*)(Pm + row64(rl, 2 * st + hh));
-      const bf16x8 p1 = *(const bf16x8*)(Pm + row64(32 + rl, 2 * st + hh));
+      const bf16x8 p0 = *(const bf16x8*)(Pm + row64(tr, 2 * st + hh));
 #pragma unroll
       for (int b = 0; b < CBW; ++b) {
-        const int c = 32 * (CBW * w + b) + rl;
+        const int c = 32 * (CBW * wq + b) + rl;
         const bf16x8 vf = *(const bf16x8*)(sm + R_VT + row64(c, 2 * st + hh));
-        acc[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p0, acc[b][0], 0, 0, 0);
-        acc[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p1, acc[b][1], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p0, acc[b], 0, 0, 0);
       }
     }
-    // hn is dead since phase 2: O goes to its rows. lane: query 32 j + rl, channels 32 cb + 8 g + 4 hh + e
+    // hn is dead since phase 2: O goes to its rows. lane: query tr, channels 32 cb + 8 g + 4 hh + e
 #pragma unroll
     for (int b = 0; b < CBW; ++b)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(uint2*)(sm + rowc(32 * j + rl, 4 * (CBW * w + b) + g, C * 2) + 8 * hh) =
-              uint2{pk_bf16(acc[b][j][4 * g], acc[b][j][4 * g + 1]), pk_bf16(acc[b][j][4 * g + 2], acc[b][j][4 * g + 3])};
+      for (int g = 0; g < 4; ++g)
+        *(uint2*)(sm + rowc(tr, 4 * (CBW * wq + b) + g, C * 2) + 8 * hh) =
+            uint2{pk_bf16(acc[b][4 * g], acc[b][4 * g + 1]), pk_bf16(acc[b][4 * g + 2], acc[b][4 * g + 3])};
   }
   __syncthreads();
-  // ---- 5. out = x + O Wp^T + bp: D[c'][token], wave w: blocks CBW w .. x 2 token blocks
+  // ---- 5. out = x + O Wp^T + bp: D[c'][token], wave: blocks CBW wq .. x token block wt
+  float* const spart = (float*)(sm + R_ST);  // [token block][2][C]: the two token blocks' statistics
   {
-    f32x16 acc[CBW][2];
+    f32x16 acc[CBW];
 #pragma unroll
     for (int b = 0; b < CBW; ++b)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
-    constexpr int PF = 4;
+      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
     bf16x8 aw[PF][CBW];
 #pragma unroll
     for (int p = 0; p < PF; ++p)
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) aw[p][b] = *frag(a.wp, CBW * w + b, p);
+      for (int b = 0; b < CBW; ++b) aw[p][b] = *frag(a.wp, CBW * wq + b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       bf16x8 cur[CBW];
@@ -595,65 +574,50 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
       for (int b = 0; b < CBW; ++b) cur[b] = aw[st % PF][b];
       if (st + PF < KS)
 #pragma unroll
-        for (int b = 0; b < CBW; ++b) aw[st % PF][b] = *frag(a.wp, CBW * w + b, st + PF);
-      const bf16x8 o0 = hn_frag(rl, st), o1 = hn_frag(32 + rl, st);
+        for (int b = 0; b < CBW; ++b) aw[st % PF][b] = *frag(a.wp, CBW * wq + b, st + PF);
+      const bf16x8 o0 = hn_frag(tr, st);
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) {
-        acc[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[b][0], 0, 0, 0);
-        acc[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o1, acc[b][1], 0, 0, 0);
-      }
+      for (int b = 0; b < CBW; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[b], 0, 0, 0);
     }
     bf16_t* out = a.out + (size_t)img * S * C;
 #pragma unroll
     for (int b = 0; b < CBW; ++b) {
-      const int cb = CBW * w + b;
-      float s16[16], q16[16];
+      const int cb = CBW * wq + b;
+      float v[32];
+      uint32_t wv[4][2];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int t = 32 * j + rl;
-        uint32_t wv[4][2];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = 32 * cb + 8 * g + 4 * hh;
-          const f32x4 bb = *(const f32x4*)(a.bp + c);
-          const uint2 rr = *(const uint2*)(x + (size_t)t * C + c);
-          const float v0 = acc[b][j][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
-          const float v1 = acc[b][j][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
-          const float v2 = acc[b][j][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
-          const float v3 = acc[b][j][4 * g + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
-          wv[g][0] = pk_bf16(v0, v1);
-          wv[g][1] = pk_bf16(v2, v3);
-          const float r0 = __uint_as_float(wv[g][0] << 16), r1 = __uint_as_float(wv[g][0] & 0xffff0000u);
-          const float r2 = __uint_as_float(wv[g][1] << 16), r3 = __uint_as_float(wv[g][1] & 0xffff0000u);
-          s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
-          s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
-          s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
-          s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
-        }
-#pragma unroll
-        for (int gp = 0; gp < 4; gp += 2) {
-          u32x4 o;
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
-            o[d] = sw[0];
-            o[2 + d] = sw[1];
-          }
-          *(u32x4*)(out + (size_t)t * C + 32 * cb + 8 * (gp + hh)) = o;
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * cb + 8 * g + 4 * hh;
+        const f32x4 bb = *(const f32x4*)(a.bp + c);
+        const uint2 rr = *(const uint2*)(x + (size_t)tr * C + c);
+        const float v0 = acc[b][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
+        const float v1 = acc[b][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
+        const float v2 = acc[b][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
+        const float v3 = acc[b][4 * g + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
+        wv[g][0] = pk_bf16(v0, v1);
+        wv[g][1] = pk_bf16(v2, v3);
+        const float r0 = __uint_as_float(wv[g][0] << 16), r1 = __uint_as_float(wv[g][0] & 0xffff0000u);
+        const float r2 = __uint_as_float(wv[g][1] << 16), r3 = __uint_as_float(wv[g][1] & 0xffff0000u);
+        v[4 * g + 0] = r0; v[16 + 4 * g + 0] = r0 * r0;
+        v[4 * g + 1] = r1; v[16 + 4 * g + 1] = r1 * r1;
+        v[4 * g + 2] = r2; v[16 + 4 * g + 2] = r2 * r2;
+        v[4 * g + 3] = r3; v[16 + 4 * g + 3] = r3 * r3;
       }
-      if (a.out_stats) {  // one 64-token slot per image: butterfly over the 32 token lanes
-        float v[32];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          v[e] = s16[e];
-          v[16 + e] = q16[e];
+      for (int gp = 0; gp < 4; gp += 2) {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+          o[d] = sw[0];
+          o[2 + d] = sw[1];
         }
-        auto xchg = [](float xv, auto wc) {
+        *(u32x4*)(out + (size_t)tr * C + 32 * cb + 8 * (gp + hh)) = o;
+      }
+      if (a.out_stats) {  // this token block's 32 lanes: butterfly, then the two blocks summed in order
+        auto xchg = [](float xf, auto wc) {
           constexpr int wd = decltype(wc)::value;
-          const int xi = __builtin_bit_cast(int, xv);
+          const int xi = __builtin_bit_cast(int, xf);
           int r;
           if constexpr (wd == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
           else if constexpr (wd == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
@@ -676,16 +640,21 @@ __global__ __launch_bounds__(256, 1) void attn_block_kernel(AttnBlockArgs a) {
         halve(std::integral_constant<int, 2>{});
         halve(std::integral_constant<int, 1>{});
         const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
-        a.out_stats[((long long)img * 2 + (rl >> 4)) * C + co] = v[0];
+        spart[(wt * 2 + (rl >> 4)) * C + co] = v[0];
       }
     }
+  }
+  if (a.out_stats) {
+    __syncthreads();
+    for (int i = tid; i < 2 * C; i += 512)  // (sum | sum of squares) x channel: token block 0 + block 1
+      a.out_stats[(long long)img * 2 * C + i] = spart[i] + spart[2 * C + i];
   }
 }
 
 hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
-  if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(256), 0, s, a);
-  else if (C == 256) ITSD_LAUNCH(attn_block_kernel<256>, dim3(a.n), dim3(256), 0, s, a);
-  else if (C == 128) ITSD_LAUNCH(attn_block_kernel<128>, dim3(a.n), dim3(256), 0, s, a);
+  if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 256) ITSD_LAUNCH(attn_block_kernel<256>, dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 128) ITSD_LAUNCH(attn_block_kernel<128>, dim3(a.n), dim3(512), 0, s, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -205,7 +205,7 @@ class NativeUNet:
         kinds = np.zeros(max_ops, np.int32)
         ms = np.zeros(max_ops, np.float64)
         fl = np.zeros(max_ops, np.float64)
-        sh = np.zeros((max_ops, 6), np.int32)
+        sh = np.zeros((max_ops, 8), np.int32)
         n = ctypes.c_int()
         check(lib().itsd_profile_ops(self.h, x.data_ptr(), t.data_ptr(), x.shape[0], max_ops,
                                      kinds.ctypes.data, ms.ctypes.data, fl.ctypes.data, sh.ctypes.data,
@@ -223,7 +223,7 @@ class NativeUNet:
         dec = [decode(int(kinds[i])) for i in range(k)]
         return [{"kind": dec[i][0], "kernel": dec[i][1], "ms": float(ms[i]), "flops": float(fl[i]),
                  "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
-                 "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5])} for i in range(k)]
+                 "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5]), "op": int(sh[i, 6])} for i in range(k)]
 
 
 def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset: int = 0,

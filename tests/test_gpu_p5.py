@@ -117,3 +117,27 @@ def test_p5_census_4x4_level_fused():
     print({o["kernel"] for o in at4})
     assert len(p5) == 14  # block1 + block2 of the 7 ResBlocks at 4x4 (2 down, 2 middle, 3 up)
     assert len(gn) == 1   # the middle AttnBlock's GroupNorm (materialised for the q|k|v conv)
+
+
+def test_p5_gn_fold_vs_gn_coef_launches():
+    """gn_fold: conv3x3_gn_p5_kernel reduces its input's statistics slabs to group mean / rstd itself
+    (fp64, as gn_coef_kernel) and the gn_coef launch before it is skipped; the forward equals the
+    unfolded one to the last bits of the fp64 group sums (rel-L2 <= 1e-3)."""
+    net = _net()
+    n = 32
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    xd, td = x.cuda(), t.cuda()
+    folded = _eps(net, xd, td)
+    rt.set_option("gn_fold", 0)
+    try:
+        plain = _eps(net, xd, td)
+        ops0 = net.native(n).profile_ops(xd, td.to(torch.int32))
+    finally:
+        rt.set_option("gn_fold", 1)
+    ops1 = net.native(n).profile_ops(xd, td.to(torch.int32))
+    c0 = sum(o["kind"] == "gncoef" for o in ops0)
+    c1 = sum(o["kind"] == "gncoef" for o in ops1)
+    print(f"gn_coef launches: {c0} unfolded, {c1} folded; rel-L2 {_rel_l2(folded, plain):.2e}")
+    assert c1 < c0 - 30 and _rel_l2(folded, plain) < 1e-3

@@ -40,7 +40,7 @@ sel = [int(v) for v in sys.argv[2:]] or [i for i, o in enumerate(ops) if o["kind
 for i in sel:
     o = ops[i]
     L.itsd_set_option(b"conv_dbg", int(os.environ.get("ITSD_DBG", "0")))
-    ms = nat.profile_op(x, t, i, reps=3)
+    ms = nat.profile_op(x, t, o["op"], reps=3)
     buf = np.zeros(1024 * 128, dtype=np.uint64)
     assert L.itsd_debug_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))) == 0
     st = buf.reshape(1024, 16, 8).astype(np.float64)
