@@ -43,6 +43,7 @@ int g_option_gen = 0;  // bumped by every itsd_set_option: part of the step-grap
 bool conv_gn_eligible(int H, int W);
 bool p5_eligible(int H, int W);
 bool conv_p5_selected(const ConvArgs& a);
+bool conv_p4_selected(const ConvArgs& a);
 int conv_gn_wide_segs(int H, int W, int M, int Cout);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
@@ -776,9 +777,10 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
       if (a.C1 % epc || a.C2 % epc || a.Cout % 4 || a.K % epc)
         return fail(ITSD_ERR_INVALID, "conv channels must be multiples of " + std::to_string(epc));
     }
-  // gn_fold: conv3x3_gn_p5_kernel reduces the input's statistics slabs itself (run_program then
-  // skips the op's gn_coef launch)
-  if (a.gn_coef && o.gn_gamma != SIZE_MAX && itsd::g_gn_fold && (a.C1 + a.C2) % 128 == 0 && conv_p5_selected(a)) {
+  // gn_fold: conv3x3_gn_p5_kernel / conv3x3_gn_p4_kernel reduce the input's statistics slabs themselves
+  // (run_program then skips the op's gn_coef launch)
+  if (a.gn_coef && o.gn_gamma != SIZE_MAX && itsd::g_gn_fold && (a.C1 + a.C2) % 128 == 0 &&
+      (conv_p5_selected(a) || conv_p4_selected(a))) {
     a.gn_fold = 1;
     a.gn_st1 = (const float*)(u->ws + u->acts[o.src1].stats);
     a.gn_st2 = o.src2 >= 0 ? (const float*)(u->ws + u->acts[o.src2].stats) : nullptr;

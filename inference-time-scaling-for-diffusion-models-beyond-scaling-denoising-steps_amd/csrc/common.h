@@ -21,7 +21,7 @@ extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
-extern int g_gn_fold;       // GroupNorm finalize inside p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
+extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 // Census (itsd_profile_ops): the first kernel an op launches. Every launch site goes through
 // ITSD_LAUNCH, which records the kernel expression's name if none is recorded yet; the census
@@ -133,7 +133,7 @@ struct ConvArgs {
   // are zero between launches (zeroed at create, reset by each last arriver)
   int ksplit;
   int* tickets;
-  // the GroupNorm finalize folded into conv3x3_gn_p5_kernel (gn_fold != 0: the gn_coef launch is
+  // the GroupNorm finalize folded into conv3x3_gn_p4 / p5_kernel (gn_fold != 0: the gn_coef launch is
   // skipped and the halo waves reduce the input's statistics slabs to group mean / rstd themselves)
   int gn_fold;
   const float* gn_st1;

@@ -1020,7 +1020,16 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #define STAMP(var) const unsigned long long var = stamp()
 #define STAMP_ADD(slot, d) st[slot] += (d)
+// timeline stamps (s_memrealtime, 100 MHz, one clock for every block and launch): slot s of wave w
+__device__ __forceinline__ void tl_stamp(int slot) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) g_stamps[((blockIdx.x & 1023) * 16 + (threadIdx.x >> 6)) * 8 + slot] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+#define TL(slot) tl_stamp(slot)
 #else
+#define TL(slot)
 #define STAMP(var)
 #define STAMP_ADD(slot, d)
 #endif
@@ -1144,7 +1153,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
   constexpr int RING = (AB & 64) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
   static_assert(36 % RING == 0, "ring slots repeat per chunk");
-  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4];
+  // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4 + 4 * 64 * 4];
   char* const rlds = smem + 2 * HALO;
   float* const addv = (float*)(smem + 2 * HALO + RESB);  // [2 tile parities][NSEG][128]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1153,10 +1163,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
   const int nTC = a.Cout / CONV_BM, NT = (a.M / GNW_BN) * nTC;
   const int G = gridDim.x, b = blockIdx.x;
-  const int ntiles = b < NT ? (NT - 1 - b) / G + 1 : 0;
+  // block b walks the contiguous tile range [tb0, tb0 + ntiles) (cout tile fastest): its tiles share
+  // pixel tiles and images, so a gn_fold block reduces an image's statistics once for all of them
+  const int tb0 = (int)(((long long)b * NT) / G);
+  const int ntiles = (int)(((long long)(b + 1) * NT) / G) - tb0;
   const int nstages = ntiles * ncc;
-  auto tile_p = [&](int k) { return ((b + k * G) / nTC) * GNW_BN; };
-  auto tile_c = [&](int k) { return ((b + k * G) % nTC) * CONV_BM; };
+  auto tile_p = [&](int k) { return ((tb0 + k) / nTC) * GNW_BN; };
+  auto tile_c = [&](int k) { return ((tb0 + k) % nTC) * CONV_BM; };
 #ifdef ITSD_STAMPS
   // MFMA waves: 0 chunk compute, 1 barrier wait, 6 epilogues, 7 total; halo waves: 3 stage
   // transforms (incl. next-stage load issue), 1 barrier wait, 5 prologue (stage 0), 7 total
@@ -1617,6 +1630,51 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   };
   int ipix[ITEMS];
   const float* cbase;  // GroupNorm coefficients of the loading tile's image, this lane's 8 channels
+  int simg = 0;        // (gn_fold) the loading tile's image of this thread's segment
+  int gimg = -1;       // (gn_fold) the image whose statistics gsw holds
+  float* const gsw = (float*)(smem + 2 * HALO + RESB + 2 * NSEG * CONV_BM * 4) + (wid - 4) * 64;
+  // gn_fold (conv3x3_gn_p5_kernel's reduction): group mean / rstd of image img from the producers'
+  // statistics slabs, fp64, this wave's 32 groups -> gsw. Lane = (group lane & 31, half lane >> 5);
+  // its (channel pair, slot) items in batches of 8 with all 16 loads in flight before the first sum
+  auto group_stats = [&](int img) __attribute__((always_inline)) {
+    const int g = lane & 31, hf = Cin / 64, c0 = g * 2 * hf + (lane >> 5) * hf;
+    const int HWi = H * W;
+    const int sp1 = stat_spi(HWi, a.gn_spi1), sp2 = a.C2 ? stat_spi(HWi, a.gn_spi2) : 0;
+    const int spm = sp1 > sp2 ? sp1 : sp2, np = hf >> 1, m = np * spm;
+    double sm = 0.0, sq = 0.0;
+    for (int b0 = 0; b0 < m; b0 += 8) {
+      float2 vs[8], vq[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int it = b0 + i, q = it / np, cr = c0 + 2 * (it - q * np);
+        const bool s1 = cr < a.C1;
+        const bool ok = it < m && q < (s1 ? sp1 : sp2);
+        const int c = ok ? cr : c0, qq = ok ? q : 0;
+        const bool t1 = c < a.C1;
+        const float* st = t1 ? a.gn_st1 : a.gn_st2;
+        const int Cs = t1 ? a.C1 : a.C2, cs = t1 ? c : c - a.C1, sp = t1 ? sp1 : sp2;
+        const long long slot = (long long)img * sp + qq;
+        const float2 u0 = *(const float2*)(st + (slot * 2) * Cs + cs);
+        const float2 u1 = *(const float2*)(st + (slot * 2 + 1) * Cs + cs);
+        vs[i] = ok ? u0 : float2{0.f, 0.f};
+        vq[i] = ok ? u1 : float2{0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sm += (double)vs[i].x + (double)vs[i].y;
+        sq += (double)vq[i].x + (double)vq[i].y;
+      }
+    }
+    sm += __shfl_xor(sm, 32, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    const double E = (double)(Cin / 32) * HWi, mean = sm / E;
+    double var = sq / E - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    if (lane < 32) {
+      gsw[2 * g] = (float)mean;
+      gsw[2 * g + 1] = (float)(1.0 / sqrt(var + 1e-5));
+    }
+  };
   auto geometry_pix = [&](int k) __attribute__((always_inline)) {
     int img0, y0;
     tile_y0img(k, img0, y0);
@@ -1632,6 +1690,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
     }
     cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
+    simg = img0 + sg;
   };
   // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
   // address is chosen once; the other items' addresses are lds0/lds1 plus constants.
@@ -1744,30 +1803,61 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       }
     }
   };
-  u32x4 h[ITEMS];
-  f32x4 c[4], cn[4];
-  auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) c[q][e] = cn[q][e] * GN_L2E;
-  };
   // the stage being loaded: tile kL, chunk ccL (the emitted stage is the one before it)
   int kL = 0, ccL = 0;
+  u32x4 h[ITEMS];
+  f32x4 c[4], cn[4];
+  // the loaded stage's coefficients c from cn: gn_coef rows (a0..a7, b0..b7), or (gn_fold) gamma0..7,
+  // beta0..7 with the group statistics in gsw: a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula)
+  auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
+    if (a.gn_fold) {
+      // group of channel c = floor((c + 0.5) / gsz) by a reciprocal (exact: c < 2^11, gsz <= 64)
+      const int c0 = ccL * 64 + 8 * lch;
+      const float rg = 32.0f / (float)Cin;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = (int)(((float)(c0 + e) + 0.5f) * rg);
+        const float mean = gsw[2 * g], rstd = gsw[2 * g + 1];
+        const float sc = rstd * cn[e >> 2][e & 3];
+        c[e >> 2][e & 3] = sc * GN_L2E;
+        c[2 + (e >> 2)][e & 3] = (cn[2 + (e >> 2)][e & 3] - mean * sc) * GN_L2E;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c[q][e] = cn[q][e] * GN_L2E;
+    }
+  };
+  auto load_cn = [&](int ccx) __attribute__((always_inline)) {  // (stage coefficients or affine, as above)
+    if (a.gn_fold) {
+      const int c0 = ccx * 64 + 8 * lch;
+      cn[0] = *(const f32x4*)(a.gn_gamma + c0);
+      cn[1] = *(const f32x4*)(a.gn_gamma + c0 + 4);
+      cn[2] = *(const f32x4*)(a.gn_beta + c0);
+      cn[3] = *(const f32x4*)(a.gn_beta + c0 + 4);
+    } else {
+      const f32x4* cp = (const f32x4*)(cbase + ccx * 128);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+    }
+  };
   // transform the emitted stage (items in h, coefficients in c) into hbuf; each item's register
   // is reloaded with the loaded stage's item right after its transform; that stage's
   // coefficients go to cn first (older than every item reload: waiting for them never waits for
   // an item).
   auto emit = [&](char* hbuf) __attribute__((always_inline)) {
     if (ccL == 0) geometry_emit(kL);  // the emitted stage opens tile kL
+    bool opened = false;
     if (++ccL == ncc) {
       ccL = 0;
-      if (++kL < ntiles) geometry_pix(kL);
+      if (++kL < ntiles) {
+        geometry_pix(kL);
+        opened = true;
+      }
     }
     const bool live = kL < ntiles;
-    const f32x4* cp = (const f32x4*)(cbase + (live ? ccL : 0) * 128);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+    load_cn(live ? ccL : 0);
     const Src nx = src_of(ccL, live);
     typedef __attribute__((ext_vector_type(2))) float f32x2;
     typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
@@ -1788,18 +1878,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(nx.rs, __umul24((uint32_t)ipix[j], nx.rowb) + lch * 16, nx.so, 0);
     }
+    // gn_fold: a tile opened -- its image's group statistics (loads issued after the item reloads; the
+    // wait also covers those, inside the current MFMA stage)
+    if (a.gn_fold && opened && simg != gimg) {
+      group_stats(simg);
+      gimg = simg;
+    }
     prescale();
   };
   // prologue: stage 0 (and tile 0's addv)
   geometry_pix(0);
   {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cn[q] = ((const f32x4*)cbase)[q];
-    prescale();
+    load_cn(0);
     const Src s0 = src_of(0, true);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(s0.rs, __umul24((uint32_t)ipix[j], s0.rowb) + lch * 16, s0.so, 0);
+    if (a.gn_fold) group_stats(simg);  // (its loads in flight with stage 0's)
+    gimg = simg;
+    prescale();
   }
   emit(smem);
 #ifdef ITSD_STAMPS
@@ -1882,6 +1979,7 @@ template <int W> struct Gp5Cfg {
   static constexpr int HALO = ((NSEG * HS * ROWB) + 1023) & ~1023;  // one halo buffer (bytes)
 };
 constexpr int P5_RING = 9;  // A k-step slots (prefetch distance 8 k-steps = 32 MFMAs); divides 36
+                            // (12 and 18 measured equal at N = 32 and 256)
 constexpr int P5_BD = 3;    // B fragment buffers (reads two k-steps = 8 MFMAs ahead)
 
 template <int W>
@@ -1897,6 +1995,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   float* const addv = (float*)(smem + 2 * HALO);  // [item parity][image of the tile][128 couts]
   // gn_fold: per halo wave, [item parity][segment of the wave][32 groups][mean, rstd]
   float* const gsw_all = (float*)(smem + 2 * HALO + 2 * NSEG * CONV_BM * 4);
+  TL(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
@@ -1950,6 +2049,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
     }
     block_sync();  // B0: stage 0 staged
+    TL(1);
     int q = 0;
     for (int k = 0; k < nit; ++k) {
       int tp, tc, z;
@@ -2000,8 +2100,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc[j], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
+        if (q == 0) TL(6);
         block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
+        if (q == 0) TL(7);
       }
+      TL(2);
       // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines
       const int tile = tc * nTP + tp;
       if (S > 1) {
@@ -2041,6 +2144,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             }
         }
       }
+      TL(3);
       // ---- epilogue: out = acc + addv + residual (lane: pixel 32j + rl, couts 32w + 8g + 4hh + e)
       const int tileP = tp * 128, tileC = tc * CONV_BM;
       const float* av = addv + (k & 1) * NSEG * CONV_BM + wid * 32 + 4 * hh;
@@ -2140,7 +2244,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
         }
       }
+      TL(4);
     }
+    TL(5);
     return;
   }
 
@@ -2197,20 +2303,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     const int g = lane & 31, hf = Cin / 64, c0 = g * 2 * hf + (lane >> 5) * hf;  // (Cin / 32 channels a group)
     const int sp1 = stat_spi(HW, a.gn_spi1), sp2 = a.C2 ? stat_spi(HW, a.gn_spi2) : 0;
     const int spm = sp1 > sp2 ? sp1 : sp2;
-#pragma unroll
+    // this lane's (channel pair p, slot q) items, it = q * np + p, in batches of 8 whose 16 loads are
+    // all in flight before the first is summed (one memory round trip per batch: 1 at the 16x16 and
+    // smaller levels, 1-3 at 32x32 -- a loop over slots waited for each slot in turn)
+    const int np = hf >> 1, m = np * spm;
+#pragma unroll 1
     for (int segl = 0; segl < SEGW; ++segl) {
       const int img = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sw0 + segl;
       const int imgc = img < nimg ? img : nimg - 1;
       double sm = 0.0, sq = 0.0;
-      for (int q = 0; q < spm; ++q)
-      for (int cb0 = 0; cb0 < hf; cb0 += 16) {  // passes of 16 channels of the half group (hf = Cin / 64, even)
+      for (int b0 = 0; b0 < m; b0 += 8) {
         float2 vs[8], vq[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int cr = c0 + cb0 + 2 * i;
+          const int it = b0 + i, q = it / np, cr = c0 + 2 * (it - q * np);
           const bool s1 = cr < a.C1;
-          const int spi = s1 ? sp1 : sp2;
-          const bool ok = cb0 + 2 * i < hf && q < spi;
+          const bool ok = it < m && q < (s1 ? sp1 : sp2);
           const int c = ok ? cr : c0, qq = ok ? q : 0;
           const bool t1 = c < a.C1;
           const float* st = t1 ? a.gn_st1 : a.gn_st2;
@@ -2255,7 +2363,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       zmn |= (uint32_t)(img < nimg && y >= 0 && y < W) << j;  // (square images: H = W)
     }
     cbase = a.gn_coef + ((size_t)imgc * (Cin / 8) + lch) * 16;
-    if (a.gn_fold) group_stats(k);
   };
   // stage L's GroupNorm+SiLU coefficients of this lane's 8 channels (gn_fold: gamma / beta, turned
   // into a, b by prescale from the wave's group statistics)
@@ -2274,11 +2381,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   };
   auto prescale = [&]() __attribute__((always_inline)) {
     if (a.gn_fold) {  // a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula), per channel's group
-      const int c0 = ccL * 64 + 8 * lch, gsz = Cin / 32;
+      const int c0 = ccL * 64 + 8 * lch;
+      const float rg = 32.0f / (float)Cin;  // group = floor((c + 0.5) / gsz) (exact: c < 2^11, gsz <= 64)
       const float* gs = gsw + ((kL & 1) * SEGW + sl) * 64;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int g = (c0 + e) / gsz;
+        const int g = (int)(((float)(c0 + e) + 0.5f) * rg);
         const float mean = gs[2 * g], rstd = gs[2 * g + 1];
         const float sc = rstd * cn[e >> 2][e & 3];
         c[e >> 2][e & 3] = sc * GN_L2E;
@@ -2295,8 +2403,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   bool more = true;  // a stage L exists
   auto advance = [&]() __attribute__((always_inline)) {  // L <- the stage after L
     if (++ccL == c1L) {
-      if (++kL < nit) open_item(kL);
-      else more = false;
+      if (++kL < nit) {
+        open_item(kL);
+        if (a.gn_fold) group_stats(kL);
+      } else {
+        more = false;
+      }
     }
   };
   // emit: transform stage E (h, c, zm) into hbuf, reloading each item's register with stage L's
@@ -2338,6 +2450,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     }
   };
   // prologue: stage 0 into buffer 0 (stage 1 loading)
+  // prologue: stage 0's input and affine loads are in flight before the first item's statistics
+  // loads (one memory round trip for all of them)
   open_item(0);
   load_stage();
   {
@@ -2347,10 +2461,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(
           s0.rs, __umul24(((zmn >> j) & 1) ? (uint32_t)(pix0 + RPP * j) : 0u, s0.rowb) + lch * 16, s0.so, 0);
   }
+  if (a.gn_fold) group_stats(0);
+  TL(1);
   prescale();
   advance();
   emit(smem);
+  TL(2);
   block_sync();  // B0
+  TL(3);
   // during MFMA stage q (item k, chunk cc): stage item k's addv with its first chunk, emit stage q+1
   int q = 0;
   for (int k = 0; k < nit; ++k) {
@@ -2360,9 +2478,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     for (int cc = c0; cc < c1; ++cc, ++q) {
       if (cc == c0) stage_addv(k);
       if (!(k + 1 == nit && cc + 1 == c1)) emit(smem + ((q + 1) & 1) * HALO);
+      if (q == 0) TL(4);
       block_sync();  // end of MFMA stage q
+      if (q == 0) TL(6);
     }
   }
+  TL(5);
 }
 
 // GroupNorm finalize for the fused conv (the statistics half of gn_apply_kernel): per
@@ -2605,6 +2726,14 @@ static int p5_split(const ConvArgs& a, int tiles, int nch) {
   return S;
 }
 
+bool conv_p5_selected(const ConvArgs& a);
+// launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p4_kernel (any form)?
+bool conv_p4_selected(const ConvArgs& a) {
+  if (!a.gn_coef || conv_p5_selected(a) || !conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
+  return g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
+         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
+}
+
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p5_kernel?
 bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
@@ -2681,9 +2810,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       // the 4x4 level always (no other fused kernel holds it); the others where p4 under-fills the chip
       if (conv_p5_selected(a)) return launch_p5(a, s);
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
-        const bool p4 = g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
-                        ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
-        if (p4) {
+        if (conv_p4_selected(a)) {
           // persistent, one MFMA wave per SIMD (512 threads, 256 registers a wave)
           const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
           const dim3 gp(std::min(tiles, g_num_cus));

@@ -28,9 +28,12 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
     ap.add_argument("--fuse-gn", type=int, default=1, help="fused GroupNorm+SiLU+conv3x3 in ResBlocks")
     ap.add_argument("--io-mfma", type=int, default=1, help="bf16 head/tail on MFMA (tail GroupNorm fused)")
+    ap.add_argument("--lib", default="", help="another build of libitsd_hip.so (diagnostic variants)")
     ap.add_argument("--set", default="", help="itsd_set_option overrides for the final table, e.g. gn_wide=1+conv_dbg=2")
     args = ap.parse_args()
     from itsd import runtime as rt
+    if args.lib:
+        rt.LIB_PATH = os.path.abspath(args.lib)
     rt.set_option("fuse_gn", args.fuse_gn)
     rt.set_option("io_mfma", args.io_mfma)
     a = ARCH_A
