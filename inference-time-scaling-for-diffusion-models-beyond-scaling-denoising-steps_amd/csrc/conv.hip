@@ -1021,9 +1021,10 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define STAMP(var) const unsigned long long var = stamp()
 #define STAMP_ADD(slot, d) st[slot] += (d)
 // timeline stamps (s_memrealtime, 100 MHz, one clock for every block and launch): slot s of wave w
+// (wave 1 records s_memtime instead: the shader clock over a span = its delta / wave 0's delta x 100 MHz)
 __device__ __forceinline__ void tl_stamp(int slot) {
   __builtin_amdgcn_sched_barrier(0);
-  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t = (threadIdx.x >> 6) == 1 ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63) == 0) g_stamps[((blockIdx.x & 1023) * 16 + (threadIdx.x >> 6)) * 8 + slot] = t;
   __builtin_amdgcn_sched_barrier(0);
 }
@@ -1991,8 +1992,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   constexpr int SPX = TH * W;  // pixels of one segment
   static_assert(NSEG * SPX == 128 && ITEMS * RPP == NHY * W && ITEMS <= 31 && 36 % P5_RING == 0, "p5 geometry");
   constexpr int SEGW = 64 / TPS > 0 ? 64 / TPS : 1;  // image segments one halo wave covers (W = 4: 2)
-  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + 2 * NSEG * CONV_BM * 4 + 4 * 2 * SEGW * 64 * 4];
+  // + the residual tiles of two items [item parity][128 px][128 couts] bf16 (LDS-DMA'd by the halo waves
+  // during an item's last stage; 16-B unit u of pixel p at u ^ (p & 15))
+  constexpr int RTILE = 128 * CONV_BM * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO + 2 * NSEG * CONV_BM * 4 + 4 * 2 * SEGW * 64 * 4 + 2 * RTILE];
   float* const addv = (float*)(smem + 2 * HALO);  // [item parity][image of the tile][128 couts]
+  char* const rres = smem + 2 * HALO + 2 * NSEG * CONV_BM * 4 + 4 * 2 * SEGW * 64 * 4;
   // gn_fold: per halo wave, [item parity][segment of the wave][32 groups][mean, rstd]
   float* const gsw_all = (float*)(smem + 2 * HALO + 2 * NSEG * CONV_BM * 4);
   TL(0);
@@ -2152,6 +2157,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       float s16[16], q16[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+      const char* rk = rres + (k & 1) * RTILE;  // this item's residual tile (halo waves, before the last barrier)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int pl = j * 32 + rl, seg = pl / SPX;
@@ -2162,9 +2168,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         for (int g = 0; g < 4; ++g) {
           const int c = wid * 32 + 8 * g + 4 * hh;
           const f32x4 ad = *(const f32x4*)(avj + 8 * g);
-          const T* rp = has_res && live ? (const T*)a.resid + (size_t)(tileP + pl) * a.Cout + tileC + c
-                                        : (const T*)zero_of_block<T>(a);
-          uint2 rr = *(const uint2*)rp;
+          uint2 rr = *(const uint2*)(rk + pl * 256 + ((((c >> 3) ^ pl) & 15) << 4) + 8 * hh);
           if (!has_res) rr = uint2{0u, 0u};
           float v[4];
           v[0] = acc[j][4 * g + 0] + ad[0] + __uint_as_float(rr.x << 16);
@@ -2260,14 +2264,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     const int hrow = sg * HS + hy * W2 + (x + 1);
     lds[j] = hrow * ROWB + ((lch ^ ((hrow >> 1) & 7)) << 4);
   }
-  // the halo rows no item writes (the padding columns; interior mode: also the top and bottom rows)
-  // of both buffers: zeroed once (item writes never touch them, so no ordering against the first
-  // emit is needed; the MFMA waves read after B0)
-  for (int u = tt; u < 2 * NSEG * HS * 8; u += 256) {
-    const int row = (u >> 3) % (NSEG * HS), buf = (u >> 3) / (NSEG * HS), r = row % HS, y = r / W2, x = r - y * W2;
-    if (x == 0 || x == W2 - 1 || (!Cf::ROWS && (y == 0 || y == TH + 1)))
-      *(u32x4*)(smem + buf * HALO + row * ROWB + ((u & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
+#ifdef ITSD_STAMPS
+  {  // timeline: the kernel arguments are in SGPRs (a first dependent use)
+    int m = a.M;
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(m));
+    if (m == -1) g_stamps[0] = 0;
+    TL(7);
   }
+#endif
   const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
   const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
   struct Src {
@@ -2303,38 +2307,53 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     const int g = lane & 31, hf = Cin / 64, c0 = g * 2 * hf + (lane >> 5) * hf;  // (Cin / 32 channels a group)
     const int sp1 = stat_spi(HW, a.gn_spi1), sp2 = a.C2 ? stat_spi(HW, a.gn_spi2) : 0;
     const int spm = sp1 > sp2 ? sp1 : sp2;
-    // this lane's (channel pair p, slot q) items, it = q * np + p, in batches of 8 whose 16 loads are
-    // all in flight before the first is summed (one memory round trip per batch: 1 at the 16x16 and
-    // smaller levels, 1-3 at 32x32 -- a loop over slots waited for each slot in turn)
-    const int np = hf >> 1, m = np * spm;
-#pragma unroll 1
+    // this lane's (segment, slot q, channel pair p) items, it = (segl * spm + q) * np + p, in batches of 8
+    // whose 16 loads are all in flight before the first is summed (one memory round trip per batch: 1 at
+    // the 16x16 and smaller levels, both 4x4 segments included; 1-3 at 32x32)
+    static_assert(SEGW <= 2, "two segments a wave at most");
+    const int np = hf >> 1, m = np * spm, mt = SEGW * m;
+    int img[SEGW];
+#pragma unroll
     for (int segl = 0; segl < SEGW; ++segl) {
-      const int img = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sw0 + segl;
-      const int imgc = img < nimg ? img : nimg - 1;
-      double sm = 0.0, sq = 0.0;
-      for (int b0 = 0; b0 < m; b0 += 8) {
-        float2 vs[8], vq[8];
+      const int im = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sw0 + segl;
+      img[segl] = im < nimg ? im : nimg - 1;
+    }
+    double sm0 = 0.0, sq0 = 0.0, sm1 = 0.0, sq1 = 0.0;
+    for (int b0 = 0; b0 < mt; b0 += 8) {
+      float2 vs[8], vq[8];
+      bool hi[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int it = b0 + i, q = it / np, cr = c0 + 2 * (it - q * np);
-          const bool s1 = cr < a.C1;
-          const bool ok = it < m && q < (s1 ? sp1 : sp2);
-          const int c = ok ? cr : c0, qq = ok ? q : 0;
-          const bool t1 = c < a.C1;
-          const float* st = t1 ? a.gn_st1 : a.gn_st2;
-          const int Cs = t1 ? a.C1 : a.C2, cs = t1 ? c : c - a.C1, sp = t1 ? sp1 : sp2;
-          const long long slot = (long long)imgc * sp + qq;
-          const float2 u0 = *(const float2*)(st + (slot * 2) * Cs + cs);
-          const float2 u1 = *(const float2*)(st + (slot * 2 + 1) * Cs + cs);
-          vs[i] = ok ? u0 : float2{0.f, 0.f};
-          vq[i] = ok ? u1 : float2{0.f, 0.f};
-        }
+      for (int i = 0; i < 8; ++i) {
+        const int it = b0 + i;
+        hi[i] = SEGW > 1 && it >= m;
+        const int r = hi[i] ? it - m : it, q = r / np, cr = c0 + 2 * (r - q * np);
+        const bool s1 = cr < a.C1;
+        const bool ok = it < mt && q < (s1 ? sp1 : sp2);
+        const int c = ok ? cr : c0, qq = ok ? q : 0;
+        const bool t1 = c < a.C1;
+        const float* st = t1 ? a.gn_st1 : a.gn_st2;
+        const int Cs = t1 ? a.C1 : a.C2, cs = t1 ? c : c - a.C1, sp = t1 ? sp1 : sp2;
+        const long long slot = (long long)(hi[i] ? img[SEGW - 1] : img[0]) * sp + qq;
+        const float2 u0 = *(const float2*)(st + (slot * 2) * Cs + cs);
+        const float2 u1 = *(const float2*)(st + (slot * 2 + 1) * Cs + cs);
+        vs[i] = ok ? u0 : float2{0.f, 0.f};
+        vq[i] = ok ? u1 : float2{0.f, 0.f};
+      }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          sm += (double)vs[i].x + (double)vs[i].y;
-          sq += (double)vq[i].x + (double)vq[i].y;
+      for (int i = 0; i < 8; ++i) {
+        const double ds = (double)vs[i].x + (double)vs[i].y, dq = (double)vq[i].x + (double)vq[i].y;
+        if (hi[i]) {
+          sm1 += ds;
+          sq1 += dq;
+        } else {
+          sm0 += ds;
+          sq0 += dq;
         }
       }
+    }
+#pragma unroll
+    for (int segl = 0; segl < SEGW; ++segl) {
+      double sm = segl ? sm1 : sm0, sq = segl ? sq1 : sq0;
       sm += __shfl_xor(sm, 32, 64);
       sq += __shfl_xor(sq, 32, 64);
       const double E = (double)(Cin / 32) * HW, mean = sm / E;
@@ -2450,6 +2469,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     }
   };
   // prologue: stage 0 into buffer 0 (stage 1 loading)
+  // item k's residual tile -> rres[k & 1] by LDS-DMA: wave hw, instruction i covers tile rows
+  // 4 (8 hw + i) .. +3, lane l -> row + l / 16, LDS unit l % 16 <- source unit (l % 16) ^ (row & 15)
+  auto res_dma = [&](int k) __attribute__((always_inline)) {
+    int tp, tc, z;
+    item_of(k, tp, tc, z);
+    const int hw = (tid >> 6) - 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r0 = 4 * (8 * hw + i), r = r0 + (lane >> 4), u = (lane & 15) ^ (r & 15), p = tp * 128 + r;
+      const T* src = p < a.M ? (const T*)a.resid + (size_t)p * a.Cout + tc * CONV_BM + u * 8 : (const T*)zero_of_block<T>(a);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(rres + (k & 1) * RTILE + r0 * 256), 16, 0, 0);
+    }
+  };
   // prologue: stage 0's input and affine loads are in flight before the first item's statistics
   // loads (one memory round trip for all of them)
   open_item(0);
@@ -2460,6 +2492,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     for (int j = 0; j < ITEMS; ++j)
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(
           s0.rs, __umul24(((zmn >> j) & 1) ? (uint32_t)(pix0 + RPP * j) : 0u, s0.rowb) + lch * 16, s0.so, 0);
+  }
+  // (after stage 0's loads are issued) the halo rows no item writes (the padding columns; interior mode: also the top and bottom rows)
+  // of both buffers: zeroed once (item writes never touch them, so no ordering against the first
+  // emit is needed; the MFMA waves read after B0)
+  for (int u = tt; u < 2 * NSEG * HS * 8; u += 256) {
+    const int row = (u >> 3) % (NSEG * HS), buf = (u >> 3) / (NSEG * HS), r = row % HS, y = r / W2, x = r - y * W2;
+    if (x == 0 || x == W2 - 1 || (!Cf::ROWS && (y == 0 || y == TH + 1)))
+      *(u32x4*)(smem + buf * HALO + row * ROWB + ((u & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
   }
   if (a.gn_fold) group_stats(0);
   TL(1);
@@ -2477,7 +2517,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     const int c0 = chunk_lo(z), c1 = chunk_lo(z + 1);
     for (int cc = c0; cc < c1; ++cc, ++q) {
       if (cc == c0) stage_addv(k);
-      if (!(k + 1 == nit && cc + 1 == c1)) emit(smem + ((q + 1) & 1) * HALO);
+      // the item's residual, during its last stage; landed before that stage's barrier (only the next
+      // stage's ITEMS item reloads, issued after it, may still be in flight: loads retire in order)
+      const bool rdma = a.resid && cc + 1 == c1;
+      if (rdma) res_dma(k);
+      const bool em = !(k + 1 == nit && cc + 1 == c1);
+      if (em) emit(smem + ((q + 1) & 1) * HALO);
+      if (rdma) {
+        if (em) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ITEMS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       if (q == 0) TL(4);
       block_sync();  // end of MFMA stage q
       if (q == 0) TL(6);

@@ -74,7 +74,14 @@ def main():
         row("mfma split-K combined", 0, 3)
         row("mfma epilogue done", 0, 4)
         row("mfma exit", 0, 5)
+        d_rt = (st[:, 0, 2] - st[:, 0, 1]).astype(np.float64)
+        d_mt = (st[:, 1, 2] - st[:, 1, 1]).astype(np.float64)
+        ok = (d_rt > 0) & (d_mt > 0)
+        if ok.any():
+            print(f"   shader clock over the K loop (wave 1 memtime / wave 0 realtime): "
+                  f"{np.median(d_mt[ok] / d_rt[ok]) * 0.1:.2f} GHz")
         row("halo entry", 4, 0)
+        row("halo kernargs in SGPRs", 4, 7)
         row("halo item 0 opened", 4, 1)
         row("halo stage 0 emitted", 4, 2)
         row("halo after B0", 4, 3)
