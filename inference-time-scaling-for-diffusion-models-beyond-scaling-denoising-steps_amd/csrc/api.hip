@@ -778,8 +778,10 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
         return fail(ITSD_ERR_INVALID, "conv channels must be multiples of " + std::to_string(epc));
     }
   // gn_fold: conv3x3_gn_p5_kernel / conv3x3_gn_p4_kernel reduce the input's statistics slabs themselves
-  // (run_program then skips the op's gn_coef launch)
-  if (a.gn_coef && o.gn_gamma != SIZE_MAX && itsd::g_gn_fold && (a.C1 + a.C2) % 128 == 0 &&
+  // (run_program then skips the op's gn_coef launch); up to 8 slots an image (32x32): the 32 slots of a
+  // 64x64 image made the in-kernel reduction 4-12 dependent load batches (measured: the 64x64 level
+  // 0.90 ms folded vs 0.55 ms with its gn_coef launches, C4 at N = 16)
+  if (a.gn_coef && o.gn_gamma != SIZE_MAX && itsd::g_gn_fold && (a.C1 + a.C2) % 128 == 0 && in.H * in.W <= 1024 &&
       (conv_p5_selected(a) || conv_p4_selected(a))) {
     a.gn_fold = 1;
     a.gn_st1 = (const float*)(u->ws + u->acts[o.src1].stats);

@@ -2042,6 +2042,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       return (const char*)a.wfrag + (size_t)(tc * 4 + wid) * ablk + (size_t)cc * 4 * 1024 + lane * 16;
     };
     auto load_a = [&](const char* base, int st, u32x4& dst) __attribute__((always_inline)) {
+#if defined(ITSD_DIAG) && defined(P5_AB)
+      if constexpr ((P5_AB & 8) != 0) {  // ablation: no A loads
+        dst = u32x4{(uint32_t)st, 0u, 0u, 0u};
+        return;
+      }
+#endif
       dst = *(const u32x4*)(base + (size_t)((st >> 2) * kpt + (st & 3)) * 1024);
     };
     f32x16 acc[4];
@@ -2086,6 +2092,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
               tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
             }
           }
+#if defined(ITSD_DIAG) && defined(P5_AB)
+          if constexpr ((P5_AB & 16) != 0) {  // ablation: no B reads
+#pragma unroll
+            for (int j = 0; j < 4; ++j) fb[buf][j] = bf16x8{(short)(st + j), 0, 0, 0, 0, 0, 0, 1};
+            return;
+          }
+#endif
 #pragma unroll
           for (int j = 0; j < 4; ++j) fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 3) << 5)));
         };
@@ -2754,7 +2767,7 @@ static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) 
 #endif
 
 // conv3x3_gn_p5_kernel: levels whose 128-pixel tiles hold whole images
-bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 || W == 32); }
+bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 || W == 32 || W == 64); }
 
 // K slices of a p5 launch: the S minimising ceil(items / CUs) x (chunks per slice + ~1.5 chunks of
 // prologue / epilogue / combine), bounded by the slab and ticket capacities
@@ -2787,7 +2800,8 @@ bool conv_p4_selected(const ConvArgs& a) {
 bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
   const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
-  return a.Wout == 4 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
+  // (4x4 and 64x64: no other persistent fused kernel holds them -- p4's 256-pixel halo does not fit at W = 64)
+  return a.Wout == 4 || a.Wout == 64 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
 }
 
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
@@ -2798,7 +2812,8 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   a.ksplit = (a.splitk_ws && a.tickets) ? p5_split(a, tiles, nch) : 1;
   const int items = tiles * a.ksplit;
   const dim3 g(std::min(items, g_num_cus));
-  if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);
+  if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p5_kernel<64>, g, dim3(512), 0, s, a);
+  else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);
   else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p5_kernel<16>, g, dim3(512), 0, s, a);
   else if (a.Wout == 8) ITSD_LAUNCH(conv3x3_gn_p5_kernel<8>, g, dim3(512), 0, s, a);
   else ITSD_LAUNCH(conv3x3_gn_p5_kernel<4>, g, dim3(512), 0, s, a);

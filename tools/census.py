@@ -22,6 +22,7 @@ from itsd.model import UNet
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--img", type=int, default=32, help="image size (64: the C4 leg's ImageNet-64 shape)")
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=3)
@@ -37,16 +38,17 @@ def main():
     rt.set_option("fuse_gn", args.fuse_gn)
     rt.set_option("io_mfma", args.io_mfma)
     a = ARCH_A
-    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision=args.precision, weights="gauss")
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=args.img, precision=args.precision,
+               weights="gauss")
     net.to("cuda:0")
     nat = net.native(args.n)
-    x = torch.randn(args.n, 3, 32, 32, device="cuda")
+    x = torch.randn(args.n, 3, args.img, args.img, device="cuda")
     t = torch.full((args.n,), 500, dtype=torch.int32, device="cuda")
     if args.variants:
         # each variant: '+'-joined itsd_set_option key=value pairs, e.g.
         # "base", "small_conv=0", "conv_variant=2+splitk=0", "conv_dbg=19"
         defaults = {"conv_variant": 2, "splitk": 1, "conv_dbg": 0, "small_conv": 1, "gn_wide": 1, "conv_wide": 0,
-                    "gn_reg": 4, "small_korder": 0, "p4_w": 7, "p4_m16": 0}
+                    "gn_reg": 4, "small_korder": 0, "p4_w": 7, "p4_m16": 0, "p5": 1, "p5_split": 0, "gn_fold": 1}
         for rnd in range(3):
             for v in args.variants.split(","):
                 opts = dict(defaults)
