@@ -2,7 +2,7 @@ set -o pipefail
 # Round measurement on one MI355X: GPU tests, PMC passes over one census forward (per-dispatch
 # table + HBM traffic of the shipped kernels), the bench line, rocprofv3 kernel stats of the same
 # bench command. Usage (GPU box): bash tools/gpu_round_bench.sh r02
-R=${1:-r02}
+R=${1:-r03}
 mkdir -p gpurun_out/$R profiles
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/$R/gpu_tests.log 2>&1 || { echo tests_fail; tail -20 gpurun_out/$R/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/$R/gpu_tests.log
