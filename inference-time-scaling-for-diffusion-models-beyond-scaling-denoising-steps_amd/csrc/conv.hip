@@ -1158,6 +1158,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4 + 4 * 64 * 4];
   char* const rlds = smem + 2 * HALO;
   float* const addv = (float*)(smem + 2 * HALO + RESB);  // [2 tile parities][NSEG][128]
+#ifdef ITSD_STAMPS
+  {  // the SIMD each wave runs on (HW_ID.SIMD_ID) -> stamp slot [block][8 + wave][1]
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+    if ((threadIdx.x & 63) == 0) g_stamps[((blockIdx.x & 1023) * 16 + 8 + (threadIdx.x >> 6)) * 8 + 1] = hw;
+  }
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.Hout;
@@ -1433,12 +1439,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int step = 0; step < 36; ++step) {
-          // this step's loads are issued ahead of its MFMAs (not sunk between them by the scheduler)
           const int pf = step + RING - 1;
           if (pf < 36) load_a(cb, pf, ra[pf % RING]);
           else load_a(nb, pf - 36, ra[pf % RING]);
           if (step + BD - 1 < 36) rd(step + BD - 1, (step + BD - 1) % BD);
-          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % RING][i]);
@@ -1446,6 +1450,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
             for (int j = 0; j < 4; ++j)
               if constexpr ((AB & 1) != 0) acc[i][j][0] += __builtin_bit_cast(float, (uint32_t)fb[step % BD][j][0] << 16) + (float)af[0];
               else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % BD][j], acc[i][j], 0, 0, 0);
+          }
+          // the step's A loads, B reads and address VALU spread over its 8 MFMA gaps (measured against all of
+          // them ahead of the MFMAs in one gap: 32x32 -1 %, 16x16 -3 %, 8x8 -1.5 %, profiles/r03b/p4_sgb_ab.txt)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          }
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -2001,6 +2024,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   // gn_fold: per halo wave, [item parity][segment of the wave][32 groups][mean, rstd]
   float* const gsw_all = (float*)(smem + 2 * HALO + 2 * NSEG * CONV_BM * 4);
   TL(0);
+#ifdef ITSD_STAMPS
+  {  // timeline: the SIMD each wave runs on (HW_ID.SIMD_ID) -> stamp slot [block][8 + wave][0]
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+    if ((threadIdx.x & 63) == 0) g_stamps[((blockIdx.x & 1023) * 16 + 8 + (threadIdx.x >> 6)) * 8] = hw;
+  }
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
@@ -2070,6 +2099,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+#if defined(ITSD_DIAG) && defined(P5_CHAINS2)  // diagnostic: 8 accumulation chains (odd k-steps apart)
+      f32x16 acc2[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.0f;
+#endif
       const char* nitem = nullptr;  // the next item's first chunk (A prefetch across the item boundary)
       if (k + 1 < nit) {
         int tp2, tc2, z2;
@@ -2115,6 +2151,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % P5_RING]);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
+#if defined(ITSD_DIAG) && defined(P5_CHAINS2)
+            if (step & 1) acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc2[j], 0, 0, 0);
+            else
+#endif
             acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc[j], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -2122,6 +2162,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
         if (q == 0) TL(7);
       }
+#if defined(ITSD_DIAG) && defined(P5_CHAINS2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += acc2[j];
+#endif
       TL(2);
       // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines
       const int tile = tc * nTP + tp;
@@ -2268,6 +2312,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   }
 
   // ================================================================== halo waves
+#if defined(ITSD_DIAG) && defined(P5_NOHALO)
+  return;  // diagnostic: the MFMA waves alone on their SIMDs (with P5_AB = 24: no operand traffic either)
+#endif
   // thread tt: 8 channels (16 B unit lch) of interior pixels (lt >> 3) + RPP j of image segment sg
   const int tt = tid - 256, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
   int lds[ITEMS];

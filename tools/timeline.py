@@ -66,6 +66,10 @@ def main():
                 return
             u = us(v[m])
             print(f"   {name:24s} n={m.sum():4d}  min {u.min():7.2f}  mean {u.mean():7.2f}  max {u.max():7.2f}")
+        simd = st[:, 8:16, 0]
+        print("   SIMD of waves 0..7 (first 4 blocks): " + "  ".join("".join(str(int(v)) for v in simd[b]) for b in range(min(4, len(simd)))))
+        p4s = buf.reshape(1024, 16, 8)[:, 8:16, 1].astype(np.int64)
+        print("   p4 (last launch) SIMD of waves 0..7 (first 4 blocks): " + "  ".join("".join(str(int(v)) for v in p4s[b]) for b in range(4)))
         row("mfma entry", 0, 0)
         row("mfma after B0", 0, 1)
         row("mfma chunk 0 computed", 0, 6)
