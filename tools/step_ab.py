@@ -1,0 +1,60 @@
+"""A/B of itsd_set_option settings on the graph-replayed sampler step (the bench's timed path), in one
+process, interleaved. Measurement tool, never part of the product.
+
+    python tools/step_ab.py --n 32 --variants "base,sc_side=0" [--steps 50] [--rounds 3]
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+import itsd
+from itsd import runtime as rt
+from itsd.arch import ARCH_A
+from itsd.diffusion import GaussianDiffusionSampler
+from itsd.model import UNet
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=32)
+    ap.add_argument("--img", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="base")
+    args = ap.parse_args()
+    a = ARCH_A
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=args.img, precision="bf16",
+               weights="gauss").to("cuda:0")
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, 1000)
+    x = torch.randn(args.n, 3, args.img, args.img, device="cuda")
+    variants = args.variants.split(",")
+    res = {v: [] for v in variants}
+    for r in range(args.rounds):
+        for v in variants:
+            opts = {}
+            for kv in v.split("+"):
+                if "=" in kv:
+                    k, val = kv.split("=")
+                    opts[k] = int(val)
+            for k, val in opts.items():
+                rt.set_option(k, val)
+            smp.run(x.clone(), t_begin=999, t_end=999 - 4, seed=1)  # capture + warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            smp.run(x.clone(), t_begin=999, t_end=999 - args.steps + 1, seed=1)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / args.steps
+            res[v].append(ms)
+            for k in opts:  # back to the default of each option touched
+                rt.set_option(k, {"gn_fold": 1, "p5": 1, "p5_split": 0}.get(k, 0))
+            print(f"round {r} {v}: {ms:.4f} ms/step", flush=True)
+    for v in variants:
+        print(f"{v}: best {min(res[v]):.4f} ms/step  ({args.n * 1000 / min(res[v]) / 1000 * 1000 / 1000:.2f} cand/s at T=1000)")
+
+
+if __name__ == "__main__":
+    main()
