@@ -332,6 +332,20 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
 // 4 waves; weights (fragment-packed [Cout/32][K/16][64][8] bf16) stream from L2 into VGPRs with a
 // 4-k-step prefetch; one block per image.
 
+#ifdef ITSD_STAMPS
+// Diagnostic build only: attn_block_kernel's phase timeline (s_memrealtime), [block % 1024][wave][slot]
+__device__ unsigned long long g_stamps_attn[1024 * 16 * 8];
+__device__ __forceinline__ void atl(int slot) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) g_stamps_attn[((blockIdx.x & 1023) * 16 + (threadIdx.x >> 6)) * 8 + slot] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
+#define ATL(slot) atl(slot)
+#else
+#define ATL(slot)
+#endif
+
 template <int C>
 __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
@@ -342,6 +356,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wq = w & 3, wt = w >> 2;  // wave = (channel-block group, token block)
   const int img = blockIdx.x;
+  ATL(0);
   const bf16_t* x = a.x + (size_t)img * S * C;
   // [row][C] bf16 image, 16-B chunk ch of row r at (ch ^ (r & 15))
   auto rowc = [](int r, int ch, int rowbytes) { return r * rowbytes + ((ch ^ (r & 15)) << 4); };
@@ -382,6 +397,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
     }
   }
   __syncthreads();
+  ATL(1);  // group statistics
 #pragma unroll
   for (int i = 0; i < XU; ++i) {
     const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8), c0 = ch * 8;
@@ -406,41 +422,59 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   auto hn_frag = [&](int r, int st) { return *(const bf16x8*)(sm + rowc(r, 2 * st + hh, C * 2)); };
   const int tr = 32 * wt + rl;  // this wave's token / query row
 
-  // ---- 1. V^T: D[token][c] = hn Wv^T; wave: channel blocks CBW wq .. x token block wt
+  // The weight-streaming phases (1, 2, 5) give each wave whole 32-channel blocks over BOTH token
+  // blocks, so every weight fragment is streamed once per block (the two token-block waves of a
+  // channel group used to stream the same fragments): V^T and proj -- channel blocks w, w + 8 (NBW a
+  // wave at most); q|k -- wave w computes Q (w < 4) or K (w >= 4) of block 4 ch + w % 4. Every
+  // output's k order is unchanged.
+  constexpr int NBW = (CB + 7) / 8;
+  // ---- 1. V^T: D[token][c] = hn Wv^T; wave w: channel blocks w + 8 b x both token blocks
   {
-    f32x16 acc[CBW];
+    f32x16 acc[2][NBW];
 #pragma unroll
-    for (int b = 0; b < CBW; ++b)
+    for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-    bf16x8 bw[PF][CBW];
+      for (int b = 0; b < NBW; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tb][b][r] = 0.f;
+    bf16x8 bw[PF][NBW];
 #pragma unroll
     for (int p = 0; p < PF; ++p)
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) bw[p][b] = *frag(a.wqkv, 2 * CB + CBW * wq + b, p);
+      for (int b = 0; b < NBW; ++b)
+        if (w + 8 * b < CB) bw[p][b] = *frag(a.wqkv, 2 * CB + w + 8 * b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
-      bf16x8 cur[CBW];
+      bf16x8 cur[NBW];
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) cur[b] = bw[st % PF][b];
+      for (int b = 0; b < NBW; ++b) cur[b] = bw[st % PF][b];
       if (st + PF < KS)
 #pragma unroll
-        for (int b = 0; b < CBW; ++b) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + CBW * wq + b, st + PF);
-      const bf16x8 h0 = hn_frag(tr, st);
+        for (int b = 0; b < NBW; ++b)
+          if (w + 8 * b < CB) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + w + 8 * b, st + PF);
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur[b], acc[b], 0, 0, 0);
+      for (int tb = 0; tb < 2; ++tb) {
+        const bf16x8 h0 = hn_frag(32 * tb + rl, st);
+#pragma unroll
+        for (int b = 0; b < NBW; ++b)
+          if (w + 8 * b < CB) acc[tb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur[b], acc[tb][b], 0, 0, 0);
+      }
     }
-    // lane: channel c = 32 cb + rl (column), tokens 32 wt + 8 g + 4 hh + e (rows)
+    // lane: channel c = 32 cb + rl (column), tokens 32 tb + 8 g + 4 hh + e (rows)
 #pragma unroll
-    for (int b = 0; b < CBW; ++b) {
-      const int c = 32 * (CBW * wq + b) + rl;
-      const float bv = a.bqkv[2 * C + c];
+    for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *(uint2*)(sm + R_VT + row64(c, 4 * wt + g) + 8 * hh) =
-            uint2{pk_bf16(acc[b][4 * g] + bv, acc[b][4 * g + 1] + bv), pk_bf16(acc[b][4 * g + 2] + bv, acc[b][4 * g + 3] + bv)};
-    }
+      for (int b = 0; b < NBW; ++b) {
+        if (w + 8 * b >= CB) continue;
+        const int c = 32 * (w + 8 * b) + rl;
+        const float bv = a.bqkv[2 * C + c];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(uint2*)(sm + R_VT + row64(c, 4 * tb + g) + 8 * hh) =
+              uint2{pk_bf16(acc[tb][b][4 * g] + bv, acc[tb][b][4 * g + 1] + bv), pk_bf16(acc[tb][b][4 * g + 2] + bv, acc[tb][b][4 * g + 3] + bv)};
+      }
   }
+  ATL(2);  // hn staged + V^T computed (wave's own)
   // ---- 2. Q_c, K_c per 128-channel chunk; S^T (keys x queries) tile w (waves 0..3) in registers
   f32x16 sacc;
 #pragma unroll
@@ -448,38 +482,37 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   char* const Qc = sm + R_QK;
   char* const Kc = sm + R_QK + S * 256;
   for (int ch = 0; ch < NCH; ++ch) {
-    {
-      f32x16 aq, ak;
+    {  // wave w: Q_c (w < 4) or K_c (w >= 4), channel block 4 ch + w % 4, both token blocks
+      const int isk = w >> 2, cb = isk * CB + 4 * ch + wq;
+      f32x16 aa[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) aq[r] = ak[r] = 0.f;
-      const int cbq = 4 * ch + wq, cbk = CB + 4 * ch + wq;
-      bf16x8 fq[PF], fk[PF];
+      for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
-      for (int p = 0; p < PF; ++p) {
-        fq[p] = *frag(a.wqkv, cbq, p);
-        fk[p] = *frag(a.wqkv, cbk, p);
-      }
+        for (int r = 0; r < 16; ++r) aa[tb][r] = 0.f;
+      bf16x8 fa[PF];
+#pragma unroll
+      for (int p = 0; p < PF; ++p) fa[p] = *frag(a.wqkv, cb, p);
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
-        const bf16x8 q_ = fq[st % PF], k_ = fk[st % PF];
-        if (st + PF < KS) {
-          fq[st % PF] = *frag(a.wqkv, cbq, st + PF);
-          fk[st % PF] = *frag(a.wqkv, cbk, st + PF);
-        }
-        const bf16x8 h0 = hn_frag(tr, st);
-        aq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q_, h0, aq, 0, 0, 0);
-        ak = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k_, h0, ak, 0, 0, 0);
-      }
-      // lane: token tr (column), channels 32 wq + 8 g + 4 hh + e of the chunk (rows)
+        const bf16x8 w_ = fa[st % PF];
+        if (st + PF < KS) fa[st % PF] = *frag(a.wqkv, cb, st + PF);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int cq = 128 * ch + 32 * wq + 8 * g + 4 * hh;
-        const f32x4 bq = *(const f32x4*)(a.bqkv + cq), bk = *(const f32x4*)(a.bqkv + C + cq);
-        *(uint2*)(Qc + rowc(tr, 4 * wq + g, 256) + 8 * hh) =
-            uint2{pk_bf16(aq[4 * g] + bq[0], aq[4 * g + 1] + bq[1]), pk_bf16(aq[4 * g + 2] + bq[2], aq[4 * g + 3] + bq[3])};
-        *(uint2*)(Kc + rowc(tr, 4 * wq + g, 256) + 8 * hh) =
-            uint2{pk_bf16(ak[4 * g] + bk[0], ak[4 * g + 1] + bk[1]), pk_bf16(ak[4 * g + 2] + bk[2], ak[4 * g + 3] + bk[3])};
+        for (int tb = 0; tb < 2; ++tb) {
+          const bf16x8 h0 = hn_frag(32 * tb + rl, st);
+          aa[tb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w_, h0, aa[tb], 0, 0, 0);
+        }
       }
+      // lane: token 32 tb + rl (column), channels 32 wq + 8 g + 4 hh + e of the chunk (rows)
+      char* const dstc = isk ? Kc : Qc;
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int cq = 128 * ch + 32 * wq + 8 * g + 4 * hh, tk = 32 * tb + rl;
+          const f32x4 bq = *(const f32x4*)(a.bqkv + isk * C + cq);
+          *(uint2*)(dstc + rowc(tk, 4 * wq + g, 256) + 8 * hh) =
+              uint2{pk_bf16(aa[tb][4 * g] + bq[0], aa[tb][4 * g + 1] + bq[1]), pk_bf16(aa[tb][4 * g + 2] + bq[2], aa[tb][4 * g + 3] + bq[3])};
+        }
     }
     __syncthreads();
     if (w < 4) {
@@ -493,6 +526,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
     }
     __syncthreads();  // Q_c / K_c are rewritten by the next chunk
   }
+  ATL(3);  // scores done
   // ---- 3. softmax over keys: S[query][key] fp32 through LDS, P [query][key] bf16
   float* const Sm = (float*)(sm + R_QK);              // [64][64 + 4]
   char* const Pm = sm + R_QK + S * (S + 4) * 4;       // [64][64] bf16, 128-B rows
@@ -528,6 +562,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
               pk_bf16(v[6] * inv, v[7] * inv)};
   }
   __syncthreads();
+  ATL(4);  // softmax done
   // ---- 4. O^T = V^T P^T: D[c][query], wave: channel blocks CBW wq .. x query block wt -> O [token][C]
   {
     f32x16 acc[CBW];
@@ -554,102 +589,125 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
             uint2{pk_bf16(acc[b][4 * g], acc[b][4 * g + 1]), pk_bf16(acc[b][4 * g + 2], acc[b][4 * g + 3])};
   }
   __syncthreads();
-  // ---- 5. out = x + O Wp^T + bp: D[c'][token], wave: blocks CBW wq .. x token block wt
+  ATL(5);  // PV done
+  // ---- 5. out = x + O Wp^T + bp: D[c'][token], wave w: blocks w + 8 b x both token blocks
   float* const spart = (float*)(sm + R_ST);  // [token block][2][C]: the two token blocks' statistics
   {
-    f32x16 acc[CBW];
+    f32x16 acc[2][NBW];
 #pragma unroll
-    for (int b = 0; b < CBW; ++b)
+    for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-    bf16x8 aw[PF][CBW];
+      for (int b = 0; b < NBW; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tb][b][r] = 0.f;
+    bf16x8 aw[PF][NBW];
 #pragma unroll
     for (int p = 0; p < PF; ++p)
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) aw[p][b] = *frag(a.wp, CBW * wq + b, p);
+      for (int b = 0; b < NBW; ++b)
+        if (w + 8 * b < CB) aw[p][b] = *frag(a.wp, w + 8 * b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
-      bf16x8 cur[CBW];
+      bf16x8 cur[NBW];
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) cur[b] = aw[st % PF][b];
+      for (int b = 0; b < NBW; ++b) cur[b] = aw[st % PF][b];
       if (st + PF < KS)
 #pragma unroll
-        for (int b = 0; b < CBW; ++b) aw[st % PF][b] = *frag(a.wp, CBW * wq + b, st + PF);
-      const bf16x8 o0 = hn_frag(tr, st);
+        for (int b = 0; b < NBW; ++b)
+          if (w + 8 * b < CB) aw[st % PF][b] = *frag(a.wp, w + 8 * b, st + PF);
 #pragma unroll
-      for (int b = 0; b < CBW; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[b], 0, 0, 0);
+      for (int tb = 0; tb < 2; ++tb) {
+        const bf16x8 o0 = hn_frag(32 * tb + rl, st);
+#pragma unroll
+        for (int b = 0; b < NBW; ++b)
+          if (w + 8 * b < CB) acc[tb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[tb][b], 0, 0, 0);
+      }
     }
     bf16_t* out = a.out + (size_t)img * S * C;
 #pragma unroll
-    for (int b = 0; b < CBW; ++b) {
-      const int cb = CBW * wq + b;
-      float v[32];
-      uint32_t wv[4][2];
+    for (int tb = 0; tb < 2; ++tb) {
+      const int tk = 32 * tb + rl;  // this lane's token
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = 32 * cb + 8 * g + 4 * hh;
-        const f32x4 bb = *(const f32x4*)(a.bp + c);
-        const uint2 rr = *(const uint2*)(x + (size_t)tr * C + c);
-        const float v0 = acc[b][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
-        const float v1 = acc[b][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
-        const float v2 = acc[b][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
-        const float v3 = acc[b][4 * g + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
-        wv[g][0] = pk_bf16(v0, v1);
-        wv[g][1] = pk_bf16(v2, v3);
-        const float r0 = __uint_as_float(wv[g][0] << 16), r1 = __uint_as_float(wv[g][0] & 0xffff0000u);
-        const float r2 = __uint_as_float(wv[g][1] << 16), r3 = __uint_as_float(wv[g][1] & 0xffff0000u);
-        v[4 * g + 0] = r0; v[16 + 4 * g + 0] = r0 * r0;
-        v[4 * g + 1] = r1; v[16 + 4 * g + 1] = r1 * r1;
-        v[4 * g + 2] = r2; v[16 + 4 * g + 2] = r2 * r2;
-        v[4 * g + 3] = r3; v[16 + 4 * g + 3] = r3 * r3;
-      }
+      for (int b = 0; b < NBW; ++b) {
+        if (w + 8 * b >= CB) continue;
+        const int cb = w + 8 * b;
+        float v[32];
+        uint32_t wv[4][2];
 #pragma unroll
-      for (int gp = 0; gp < 4; gp += 2) {
-        u32x4 o;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
-          o[d] = sw[0];
-          o[2 + d] = sw[1];
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * cb + 8 * g + 4 * hh;
+          const f32x4 bb = *(const f32x4*)(a.bp + c);
+          const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
+          const float v0 = acc[tb][b][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
+          const float v1 = acc[tb][b][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
+          const float v2 = acc[tb][b][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
+          const float v3 = acc[tb][b][4 * g + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
+          wv[g][0] = pk_bf16(v0, v1);
+          wv[g][1] = pk_bf16(v2, v3);
+          const float r0 = __uint_as_float(wv[g][0] << 16), r1 = __uint_as_float(wv[g][0] & 0xffff0000u);
+          const float r2 = __uint_as_float(wv[g][1] << 16), r3 = __uint_as_float(wv[g][1] & 0xffff0000u);
+          v[4 * g + 0] = r0; v[16 + 4 * g + 0] = r0 * r0;
+          v[4 * g + 1] = r1; v[16 + 4 * g + 1] = r1 * r1;
+          v[4 * g + 2] = r2; v[16 + 4 * g + 2] = r2 * r2;
+          v[4 * g + 3] = r3; v[16 + 4 * g + 3] = r3 * r3;
         }
-        *(u32x4*)(out + (size_t)tr * C + 32 * cb + 8 * (gp + hh)) = o;
-      }
-      if (a.out_stats) {  // this token block's 32 lanes: butterfly, then the two blocks summed in order
-        auto xchg = [](float xf, auto wc) {
-          constexpr int wd = decltype(wc)::value;
-          const int xi = __builtin_bit_cast(int, xf);
-          int r;
-          if constexpr (wd == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
-          else if constexpr (wd == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
-          else if constexpr (wd == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
-          else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (wd << 10));
-          return __builtin_bit_cast(float, r);
-        };
-        auto halve = [&](auto wc) {
-          constexpr int wd = decltype(wc)::value;
-          const bool up = (rl & wd) != 0;
 #pragma unroll
-          for (int ii = 0; ii < wd; ++ii) {
-            const float lo = v[ii], hi = v[ii + wd];
-            v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+        for (int gp = 0; gp < 4; gp += 2) {
+          u32x4 o;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+            o[d] = sw[0];
+            o[2 + d] = sw[1];
           }
-        };
-        halve(std::integral_constant<int, 16>{});
-        halve(std::integral_constant<int, 8>{});
-        halve(std::integral_constant<int, 4>{});
-        halve(std::integral_constant<int, 2>{});
-        halve(std::integral_constant<int, 1>{});
-        const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
-        spart[(wt * 2 + (rl >> 4)) * C + co] = v[0];
+          *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
+        }
+        if (a.out_stats) {  // this token block's 32 lanes: butterfly, then the two blocks summed in order
+          auto xchg = [](float xf, auto wc) {
+            constexpr int wd = decltype(wc)::value;
+            const int xi = __builtin_bit_cast(int, xf);
+            int r;
+            if constexpr (wd == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+            else if constexpr (wd == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+            else if constexpr (wd == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+            else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (wd << 10));
+            return __builtin_bit_cast(float, r);
+          };
+          auto halve = [&](auto wc) {
+            constexpr int wd = decltype(wc)::value;
+            const bool up = (rl & wd) != 0;
+#pragma unroll
+            for (int ii = 0; ii < wd; ++ii) {
+              const float lo = v[ii], hi = v[ii + wd];
+              v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+            }
+          };
+          halve(std::integral_constant<int, 16>{});
+          halve(std::integral_constant<int, 8>{});
+          halve(std::integral_constant<int, 4>{});
+          halve(std::integral_constant<int, 2>{});
+          halve(std::integral_constant<int, 1>{});
+          const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
+          spart[(tb * 2 + (rl >> 4)) * C + co] = v[0];
+        }
       }
     }
   }
+  ATL(6);  // proj + epilogue (wave's own)
   if (a.out_stats) {
     __syncthreads();
     for (int i = tid; i < 2 * C; i += 512)  // (sum | sum of squares) x channel: token block 0 + block 1
       a.out_stats[(long long)img * 2 * C + i] = spart[i] + spart[2 * C + i];
   }
+  ATL(7);
 }
+
+#ifdef ITSD_STAMPS
+extern "C" int itsd_debug_stamps_attn(unsigned long long* host) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(itsd::g_stamps_attn), sizeof(unsigned long long) * 1024 * 128) == hipSuccess ? 0 : 1;
+}
+#endif
 
 hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
   if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(512), 0, s, a);
