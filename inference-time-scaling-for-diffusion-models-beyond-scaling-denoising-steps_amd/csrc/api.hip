@@ -331,6 +331,33 @@ struct Builder {
     }
     return ar.add(tmp.data(), tmp.size() * 4);
   }
+  // ConvTranspose2d(Cin, Cout, 5, stride 2, padding 2, output_padding 1) (ModelCondition.py:80) as 4
+  // sub-pixel phases: output (2m+ry, 2n+rx) = sum over input (m+dy, n+dx), dy, dx in {-1, 0, 1}, of
+  // x * w[ci][co][k(ry, dy)][k(rx, dx)] with k(0, d) = 2 - 2d, k(1, d) = 3 - 2d (none for d = -1):
+  // W'[ph][co][((dy+1)*3 + dx+1)*Cin + ci] (transposed-conv weight layout [Cin][Cout][5][5])
+  size_t pack_convt_subpix(const float* W, int Cout, int Cin) {
+    auto kk = [](int r, int d) { return r == 0 ? 2 - 2 * d : (d < 0 ? -1 : 3 - 2 * d); };
+    const int K = 9 * Cin;
+    std::vector<float> tmp((size_t)4 * Cout * K, 0.f);
+    for (int ph = 0; ph < 4; ++ph) {
+      const int ry = ph >> 1, rx = ph & 1;
+      for (int co = 0; co < Cout; ++co)
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int ky = kk(ry, dy), kx = kk(rx, dx);
+            if (ky < 0 || kx < 0 || !W) continue;
+            for (int ci = 0; ci < Cin; ++ci)
+              tmp[((size_t)ph * Cout + co) * K + ((dy + 1) * 3 + dx + 1) * Cin + ci] =
+                  W[(((size_t)ci * Cout + co) * 5 + ky) * 5 + kx];
+          }
+    }
+    if (u->bf16) {
+      std::vector<uint16_t> b(tmp.size());
+      for (size_t i = 0; i < tmp.size(); ++i) b[i] = host_f2bf(tmp[i]);
+      return ar.add(b.data(), b.size() * 2);
+    }
+    return ar.add(tmp.data(), tmp.size() * 4);
+  }
   int upconv(int s1, const std::string& name, int Cout, int Hout) {
     const Act& A = u->acts[s1];
     const int Cin = A.C, epc = u->bf16 ? 8 : 4;
@@ -595,10 +622,20 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
         cur = b.upconv(cur, p + ".main", now, 2 * Hc);
       } else {  // ConvTranspose2d(5, 2, 2, 1) then Conv 3x3, ModelCondition.py:83-85
         const float* Wt = b.get(p + ".t.weight", (int64_t)now * now * 25);
-        size_t wt = b.pack({Wt}, now, now, 5, true);
         size_t bt = b.f32(p + ".t.bias", now);
         int tmp = b.act(2 * Hc, 2 * Hc, now);
-        b.conv(cur, -1, tmp, wt, bt, now, 5, 1, 2, 0, -1, -1, 1);
+        const int epc = u->bf16 ? 8 : 4;
+        if (((Hc * Hc) % 128 == 0 || 128 % (Hc * Hc) == 0) && now % (8 * epc) == 0) {
+          // sub-pixel form: 4 phase-wise 3x3 convs over the input grid (9 of the 25 taps a phase,
+          // against 25 per output of the zero-insertion form)
+          size_t wt = b.pack_convt_subpix(Wt, now, now);
+          if (Hc * Hc < 128) u->acts[tmp].spi = 4;  // one statistics slot per (image, phase)
+          b.conv(cur, -1, tmp, wt, bt, now, 3, 1, 1, 0);
+          u->ops.back().subpix = 2;
+        } else {
+          size_t wt = b.pack({Wt}, now, now, 5, true);
+          b.conv(cur, -1, tmp, wt, bt, now, 5, 1, 2, 0, -1, -1, 1);
+        }
         cur = b.conv_layer(tmp, -1, p + ".c", now, 3, 1, 1, 0, 2 * Hc, 2 * Hc);
       }
     }
@@ -759,12 +796,12 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     }
     a.zins = o.zins;
     a.dbg = itsd::g_conv_dbg;
-    if (o.subpix) {  // input-grid GEMM with 2x2 taps per phase (conv.hip)
-      a.subpix = 1;
+    if (o.subpix) {  // input-grid GEMM with 2x2 (upsample) / 3x3 (ConvTranspose2d) taps per phase (conv.hip)
+      a.subpix = o.subpix;
       a.Hout = in.H; a.Wout = in.W;
       a.M = c.nb * in.H * in.W;
-      a.ksize = 2; a.pad = 0; a.upsample = 0;
-      a.K = 4 * (a.C1 + a.C2);
+      a.ksize = o.subpix == 2 ? 3 : 2; a.pad = o.subpix == 2 ? 1 : 0; a.upsample = 0; a.zins = 0;
+      a.K = a.ksize * a.ksize * (a.C1 + a.C2);
     }
     if (o.coef != SIZE_MAX) {
       if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
@@ -864,7 +901,9 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
 double op_flops(const itsd_unet* u, const Op& o, int nb) {
   if (o.kind == OP_CONV) {  // executed MFMA work (sub-pixel upsample convs: 4 of the 9 taps)
     const Act& out = u->acts[o.dst];
-    return 2.0 * nb * out.H * out.W * (double)o.Cout * (o.subpix ? o.K * 4 / 9 : o.K);
+    // (executed: nearest-x2 upsample convs 4 of their 9 taps per output; the sub-pixel ConvTranspose2d's
+    // K is already its 9 taps per output)
+    return 2.0 * nb * out.H * out.W * (double)o.Cout * (o.subpix == 1 ? o.K * 4 / 9 : o.K);
   }
   if (o.kind == OP_ATTN) return 2.0 * 2.0 * nb * (double)o.S * o.S * o.C;
   if (o.kind == OP_ATTNBLOCK)  // q|k|v and proj projections + the two attention products

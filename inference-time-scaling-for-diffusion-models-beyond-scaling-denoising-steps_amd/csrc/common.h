@@ -124,7 +124,8 @@ struct ConvArgs {
   // fused GroupNorm+SiLU of the input (bf16 3x3, conv3x3_gn_kernel): per-image channel
   // coefficients coef[img][Cin/8][a0..a7, b0..b7] (gn_coef_kernel); null = plain conv
   const float* gn_coef;
-  int subpix;                        // nearest-x2 upsample + 3x3 conv run as 4 phase-wise 2x2 convs
+  int subpix;                        // 1: nearest-x2 upsample + 3x3 conv run as 4 phase-wise 2x2 convs;
+                                     // 2: ConvTranspose2d(5, 2, 2, 1) as 4 phase-wise 3x3 convs (pad 1)
                                      // (grid.z = phase py*2+px): Hout/Wout/M/ksize/K describe the
                                      // input-grid GEMM; output rows are (2i+py, 2j+px) of a 2x grid
   int dbg;                           // g_conv_dbg (measurements only)

@@ -418,9 +418,10 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   const int cpt = Cin / BK;  // K-chunks per tap
   const int nK = a.ksize * a.ksize * cpt;
   const int HWo = a.Hout * a.Wout;
-  // sub-pixel phase (upsample convs): 2x2 taps at input offsets (dy + py - 1, dx + px - 1)
+  // sub-pixel phase: (subpix 1, nearest-x2 upsample convs) 2x2 taps at input offsets (dy + py - 1,
+  // dx + px - 1); (subpix 2, CFG ConvTranspose2d(5, 2, 2, 1)) 3x3 taps at (dy - 1, dx - 1) for every phase
   const int phase = a.subpix ? bt.z : -1;
-  const int padY = a.subpix ? 1 - (phase >> 1) : a.pad, padX = a.subpix ? 1 - (phase & 1) : a.pad;
+  const int padY = a.subpix == 1 ? 1 - (phase >> 1) : a.pad, padX = a.subpix == 1 ? 1 - (phase & 1) : a.pad;
   const T* wbase = (const T*)a.wt + (a.subpix ? (size_t)phase * a.Cout * a.K : 0);
   const int Hv = a.upsample ? 2 * a.Hin : (a.zins ? 2 * a.Hin - 1 : a.Hin);
   const int Wv = a.upsample ? 2 * a.Win : (a.zins ? 2 * a.Win - 1 : a.Win);
@@ -2982,7 +2983,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   const int v = g_conv_variant;
   const bool lin = !(a.upsample | a.zins);
   if (a.subpix) {
-    if (!pipe || !lin || a.ksize != 2 || ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
+    if (!pipe || !lin || a.ksize != (a.subpix == 2 ? 3 : 2) || ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
       return hipErrorInvalidValue;
     grid.z = 4;
     ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
