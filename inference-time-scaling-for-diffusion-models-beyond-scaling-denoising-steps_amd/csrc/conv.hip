@@ -539,6 +539,11 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
 // 4-deep global_load_lds ring (16 KB per stage, 3 stages in flight), 2 blocks per CU.
 // The epilogue is the shared one at 64 x 64 (host: 64 % HWo == 0, so a tile holds whole
 // images and whole GroupNorm statistics slots).
+// Split K (gridDim.z = S > 1: the 2x2 / 1x1 levels and small batches, where M / 64 x Cout / 64
+// is a handful of tiles streaming megabytes of weights): slice z runs K-chunks
+// [z nK / S, (z+1) nK / S) and hands its 64 x 64 fp32 partial to the last-arriving slice of
+// the tile (the p5 hand-off: sc1 stores, drain, ticket), which sums the S partials in slice
+// order -- bit-identical whichever slice arrives last -- and runs the epilogue.
 constexpr int SM_B = 64;                    // couts and pixels per small tile
 constexpr int SM_TILEB = SM_B * ROWB;       // 8 KB
 constexpr int SM_NS = 4;
@@ -587,7 +592,8 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
     tmask[q] = m;
   }
   const int ntap = a.ksize * a.ksize;
-  auto issue = [&](int kc) {
+  const int S = gridDim.z, kc0 = bt.z * nK / S, nKs = (bt.z + 1) * nK / S - kc0;
+  auto issue = [&](int kc, int slot) {
     int tap, ci0;
     if constexpr (TAPIN) {
       const int cc = kc / ntap;
@@ -598,7 +604,7 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       ci0 = (kc - tap * cpt) * BK;
     }
     const int ky = tap / a.ksize, kx = tap - ky * a.ksize;
-    char* sA = smem + (kc % SM_NS) * STAGE;
+    char* sA = smem + slot * STAGE;
     char* sB = sA + SM_TILEB;
     const bool s1 = ci0 < a.C1;
     const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
@@ -619,14 +625,14 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
   for (int s = 0; s < SM_NS - 1; ++s)
-    if (s < nK) issue(s);
-  for (int kc = 0; kc < nK; ++kc) {
-    const int ahead = min(SM_NS - 2, nK - 1 - kc);  // younger stages kept in flight (4 DMA each)
+    if (s < nKs) issue(kc0 + s, s);
+  for (int kc = 0; kc < nKs; ++kc) {
+    const int ahead = min(SM_NS - 2, nKs - 1 - kc);  // younger stages kept in flight (4 DMA each)
     if (ahead >= 2) wait_vmcnt<8>();
     else if (ahead == 1) wait_vmcnt<4>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    if (kc + SM_NS - 1 < nK) issue(kc + SM_NS - 1);
+    if (kc + SM_NS - 1 < nKs) issue(kc0 + kc + SM_NS - 1, (kc + SM_NS - 1) % SM_NS);
     const char* A = smem + (kc % SM_NS) * STAGE;
     const char* B = A + SM_TILEB;
     bf16x8 af[4], bf[4];
@@ -641,6 +647,46 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
   }
   wait_vmcnt<0>();
   __syncthreads();
+  if (S > 1) {
+    // partial out (slab[tile][z][g][thread] as 16-B rows), drained by every wave before thread 0
+    // takes the tile's ticket; the slice drawing S-1 resets it and sums slices 0..S-1
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+        a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
+    const int tile = bt.y * gridDim.x + bt.x;
+    const uint32_t base = (uint32_t)((size_t)tile * S * 16384) + tid * 16;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(acc[4 * g]), __float_as_uint(acc[4 * g + 1]), __float_as_uint(acc[4 * g + 2]),
+                __float_as_uint(acc[4 * g + 3])},
+          slab, base + bt.z * 16384 + g * 4096, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (flag[0] != S - 1) return;  // another slice finishes this tile (uniform over the block)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // (no instruction: keeps the loads below the ticket)
+    if (tid == 0) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 8 slices' loads in flight per batch (one memory round trip each), summed in slice order
+    for (int sl0 = 0; sl0 < S; sl0 += 8) {
+      u32x4 v[8][4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          v[j][g] = __builtin_amdgcn_raw_buffer_load_b128(slab, base + min(sl0 + j, S - 1) * 16384 + g * 4096, 0, 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (sl0 + j < S)
+              acc[4 * g + e] = sl0 + j == 0 ? __uint_as_float(v[j][g][e]) : acc[4 * g + e] + __uint_as_float(v[j][g][e]);
+    }
+    __syncthreads();  // flag read by every wave before E overwrites it
+  }
   // accumulators -> E[pixel][cout] (row SM_B + 4 floats)
   float* E = (float*)smem;
 #pragma unroll
@@ -2969,10 +3015,21 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
     // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured
     // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt)
+    // Under ~one block per CU (the 2x2 / 1x1 levels, small batches) conv_small splits K itself
+    // (in-launch combine), up to ~2 blocks per CU with >= 2 K-chunks a slice.
+    dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
+    int S = 1;
+    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk && a.Hout * a.Wout <= 16 &&
+        gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
+      const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
+      S = std::min(std::min((512 + blocks - 1) / blocks, nK / 2), 16);  // <= 2 combine batches
+      while (S > 1 && (long long)blocks * S * 4096 > a.splitk_cap) --S;
+      if (S < 1) S = 1;
+    }
     if (g_small_conv && conv_small_ok(a) &&
-        (g_small_conv == 2 ||
+        (g_small_conv == 2 || S > 1 ||
          (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
-      const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
+      gs.z = S;
       if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);
       else ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
       return hipGetLastError();

@@ -15,8 +15,8 @@ import torch
 import itsd
 
 CONV_KINDS = ("conv", "convgn", "convgnw", "convgnw4")
-from itsd.arch import ARCH_A
-from itsd.model import UNet
+from itsd.arch import ARCH_A, ARCH_C
+from itsd.model import CondUNet, UNet
 
 
 def main():
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--img", type=int, default=32, help="image size (64: the C4 leg's ImageNet-64 shape)")
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--arch", default="a", help="a: Arch A UNet; c: Arch C CondUNet (the C3 leg; --n is the guided batch 2N)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="", help="comma list of conv_variant values to A/B")
@@ -37,9 +38,14 @@ def main():
         rt.LIB_PATH = os.path.abspath(args.lib)
     rt.set_option("fuse_gn", args.fuse_gn)
     rt.set_option("io_mfma", args.io_mfma)
-    a = ARCH_A
-    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=args.img, precision=args.precision,
-               weights="gauss")
+    if args.arch == "c":
+        c = ARCH_C
+        net = CondUNet(c.T, c.num_labels, c.ch, c.ch_mult, c.num_res_blocks, 0.0, img_size=args.img,
+                       precision=args.precision, weights="gauss")
+    else:
+        a = ARCH_A
+        net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=args.img, precision=args.precision,
+                   weights="gauss")
     net.to("cuda:0")
     nat = net.native(args.n)
     x = torch.randn(args.n, 3, args.img, args.img, device="cuda")
