@@ -434,7 +434,10 @@ struct Builder {
       u->ops.back().gn_gamma = u->ops[u->ops.size() - 2].gamma;
       u->ops.back().gn_beta = u->ops[u->ops.size() - 2].beta;
     }
-    if (coef != SIZE_MAX && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
+    // (plain 3x3 stride-1 convs too: conv3x3_gn_p4_kernel's plain form, conv_p4_plain_selected)
+    const bool plain3 = coef == SIZE_MAX && ks == 3 && stride == 1 && pad == 1 && !ups && Cout % 128 == 0 &&
+                        Cin % 128 == 0 && Hout == Wout && (Hout == 32 || Hout == 16 || Hout == 8);
+    if ((coef != SIZE_MAX || plain3) && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
       u->ops.back().wfrag = pack_frag(W, Cout, Cin, ks);
     if (coef != SIZE_MAX && u->bf16 && Cout % 16 == 0 && (ks * ks * Cin) % 32 == 0 && ks == 3 && Hout >= 16)
       u->ops.back().wfrag16 = pack_frag16(W, Cout, Cin, ks);
@@ -1158,6 +1161,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p4_w")) {  // levels gn_reg = 4 applies to (bit 0 W = 8, 1 W = 16, 2 W = 32); others pws
     if (value < 0 || value > 7) return fail(ITSD_ERR_INVALID, "p4_w in [0,7]");
     itsd::g_p4_w = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p4_plain")) {  // plain 3x3 stride-1 convs on conv3x3_gn_p4_kernel (halo copies the input)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_plain in [0,1]");
+    itsd::g_p4_plain = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p5")) {  // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto, 2 always (4x4: always)

@@ -52,6 +52,7 @@ int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel ch
 int g_p4_w = 7;
 int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)         // levels conv3x3_gn_p4_kernel takes under gn_reg = 4: bit 0 W = 8, 1 W = 16, 2 W = 32
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
+int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
@@ -1196,6 +1197,8 @@ constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 M
 // 32x32x16 but a denser-clocking shape (MI355X_MICROARCH.md, DVFS item 7); RES configurations
 // (W = 32, 16) only. The halo waves are the same.
 constexpr int P16_RING = 2;  // A k32-step slots (divides the 18 k32-steps of a chunk)
+// AB: bit 1 (value 2) = plain conv3x3 (no GroupNorm+SiLU: the halo waves copy the input; shipped, the
+// CFG UpSample's 3x3 conv, conv_p4_plain_selected); the other bits are diagnostic ablations (ITSD_DIAG).
 template <int W, int AB = 0, bool M16 = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   typedef bf16_t T;
@@ -1768,7 +1771,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
       ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
     }
-    cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
+    if constexpr ((AB & 2) == 0) cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
     simg = img0 + sg;
   };
   // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
@@ -1889,6 +1892,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // the loaded stage's coefficients c from cn: gn_coef rows (a0..a7, b0..b7), or (gn_fold) gamma0..7,
   // beta0..7 with the group statistics in gsw: a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula)
   auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
+    if constexpr ((AB & 2) != 0) return;  // plain conv: no GroupNorm coefficients
     if (a.gn_fold) {
       // group of channel c = floor((c + 0.5) / gsz) by a reciprocal (exact: c < 2^11, gsz <= 64)
       const int c0 = ccL * 64 + 8 * lch;
@@ -1909,6 +1913,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     }
   };
   auto load_cn = [&](int ccx) __attribute__((always_inline)) {  // (stage coefficients or affine, as above)
+    if constexpr ((AB & 2) != 0) return;
     if (a.gn_fold) {
       const int c0 = ccx * 64 + 8 * lch;
       cn[0] = *(const f32x4*)(a.gn_gamma + c0);
@@ -2898,6 +2903,17 @@ bool conv_p4_selected(const ConvArgs& a) {
          ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
 }
 
+// A plain (no GroupNorm) 3x3 stride-1 conv on conv3x3_gn_p4_kernel<W, 2>? (the CFG UpSample's conv
+// after its ConvTranspose2d: 32x32 / 16x16 / 8x8, ModelCondition.py UpSample)
+bool conv_p4_plain_selected(const ConvArgs& a) {
+  if (!g_p4_plain || a.gn_coef || !a.wfrag || a.ksize != 3 || a.stride != 1 || a.pad != 1 || a.subpix || a.upsample ||
+      a.zins || a.vt_out || !a.zero || a.K != 9 * (a.C1 + a.C2) || a.C1 % 64 || a.C2 % 64)
+    return false;
+  if (!conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
+  return a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.Hin == a.Hout && a.C1 + a.C2 >= 128 &&
+         (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
+}
+
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p5_kernel?
 bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
@@ -3010,6 +3026,15 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     if (conv_wide_launch(a, s, &we)) return we;
   }
 #endif
+  if constexpr (sizeof(T) == 2) {
+    if (conv_p4_plain_selected(a)) {
+      const dim3 gp(std::min((a.M / GNW_BN) * (a.Cout / CONV_BM), g_num_cus));
+      if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 2>), gp, dim3(512), 0, s, a);
+      else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 2>), gp, dim3(512), 0, s, a);
+      else ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 2>), gp, dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if constexpr (sizeof(T) == 2) {
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
