@@ -754,18 +754,23 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[cb][r] = 0.f;
   const float sl2 = a.scale * 1.4426950408889634f;  // softmax via exp2
   float m = -INFINITY, l = 0.f;
-  for (int kt = 0; kt < S; kt += 32) {
+  // K fragments one key tile ahead (their load latency behind the previous tile's softmax and PV)
+  bf16x8 kf[QS];
+  auto load_k = [&](int kt) {
     const int key = kt + rl;
     const bool kv = key < S;
     const bf16_t* kp = base + (size_t)(kv ? key : 0) * C3 + C + 8 * hh;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) kf[i] = kv ? *(const bf16x8*)(kp + 16 * i) : z8;
+  };
+  load_k(0);
+  for (int kt = 0; kt < S; kt += 32) {
     f32x16 s;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
-    for (int i = 0; i < QS; ++i) {
-      const bf16x8 kf = kv ? *(const bf16x8*)(kp + 16 * i) : z8;
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[i], s, 0, 0, 0);
-    }
+    for (int i = 0; i < QS; ++i) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], s, 0, 0, 0);
+    if (kt + 32 < S) load_k(kt + 32);
     // s[r] = score(query rl, key kt + (r&3) + 8(r>>2) + 4hh) (unscaled)
     float mx = -INFINITY;
 #pragma unroll
