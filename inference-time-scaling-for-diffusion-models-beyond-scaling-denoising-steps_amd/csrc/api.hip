@@ -1163,6 +1163,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_w = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "splitk_inl")) {  // conv_pipe split-K: 1 in-launch ticket combine, 0 splitk_epilogue_kernel
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "splitk_inl in [0,1]");
+    itsd::g_splitk_inl = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p4_plain")) {  // plain 3x3 stride-1 convs on conv3x3_gn_p4_kernel (halo copies the input)
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_plain in [0,1]");
     itsd::g_p4_plain = value;

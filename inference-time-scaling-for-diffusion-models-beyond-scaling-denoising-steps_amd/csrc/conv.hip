@@ -52,6 +52,7 @@ int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel ch
 int g_p4_w = 7;
 int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)         // levels conv3x3_gn_p4_kernel takes under gn_reg = 4: bit 0 W = 8, 1 W = 16, 2 W = 32
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
+int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
@@ -524,8 +525,47 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   wait_vmcnt<0>();
   __syncthreads();
   if (S > 1) {
-    splitk_store(a, acc, z, S, bt, gridDim.x);
-    return;
+    if (!a.tickets) {  // (host: tile count above the ticket capacity) splitk_epilogue_kernel combines
+      splitk_store(a, acc, z, S, bt, gridDim.x);
+      return;
+    }
+    // in-launch combine (conv_small's hand-off): write-through partial [tile][z][16 x 4 KB rows],
+    // drained by every wave; the slice drawing ticket S-1 sums slices 0..S-1 in order
+    const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+        a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
+    const int tile = bt.y * gridDim.x + bt.x;
+    const uint32_t base = (uint32_t)((size_t)tile * S * 65536) + threadIdx.x * 16;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const f32x16& v = acc[q >> 3][(q >> 2) & 1];
+      const int g = q & 3;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(v[4 * g]), __float_as_uint(v[4 * g + 1]), __float_as_uint(v[4 * g + 2]),
+                __float_as_uint(v[4 * g + 3])},
+          slab, base + z * 65536 + q * 4096, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;
+    if (threadIdx.x == 0)
+      flag[0] = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (flag[0] != S - 1) return;  // another slice finishes this tile (uniform over the block)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // (no instruction: keeps the loads below the ticket)
+    if (threadIdx.x == 0) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int sl = 0; sl < S; ++sl) {  // (one slice's 16 loads in flight: registers beside acc)
+      u32x4 w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_raw_buffer_load_b128(slab, base + sl * 65536 + q * 4096, 0, 16);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + e];
+          acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + e] = sl == 0 ? __uint_as_float(w[q][e]) : d + __uint_as_float(w[q][e]);
+        }
+    }
+    __syncthreads();  // flag read by every wave before the epilogue reuses the LDS
   }
   if (a.dbg & 16) return;
   conv_epilogue<T>(a, acc, smem, tileP, tileC, phase);
@@ -3071,10 +3111,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
+  ConvArgs b = a;  // (conv_pipe's split-K: in-launch combine unless the tiles outnumber the tickets)
   if (pipe && v != 1 && a.splitk_ws && g_splitk) {
     // under-filled grids (the 8x8 / 4x4 levels): split K so that >= ~2 blocks per CU exist,
     // keeping >= 8 K-stages per slice
     const int blocks = (int)(grid.x * grid.y);
+    if (blocks > kTicketCap || !g_splitk_inl) b.tickets = nullptr;
     const int nK = a.ksize * a.ksize * (Cin / BK);
     int S = 1;
     if (g_splitk >= 2) S = std::min(g_splitk, nK / 4);  // forced slice count (measurements)
@@ -3083,13 +3125,13 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     grid.z = S < 1 ? 1 : S;
   }
   if (!pipe || v == 1) ITSD_LAUNCH(conv_igemm<T>, grid, dim3(256), 0, s, a);
-  else if (v == 2 && lin) ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
-  else if (v == 2) ITSD_LAUNCH((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, a);
-  else if (v == 3 && lin) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
-  else if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, a);
-  else if (lin) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
-  else ITSD_LAUNCH((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, a);
-  if (grid.z > 1) {
+  else if (v == 2 && lin) ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, b);
+  else if (v == 2) ITSD_LAUNCH((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, b);
+  else if (v == 3 && lin) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, b);
+  else if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, b);
+  else if (lin) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, b);
+  else ITSD_LAUNCH((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, b);
+  if (grid.z > 1 && pipe && v != 1 && !b.tickets) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     ITSD_LAUNCH(splitk_epilogue_kernel<T>, dim3(grid.x, grid.y), dim3(256), 0, s, a, (int)grid.z);
