@@ -15,8 +15,8 @@ Rank 0 prints ONE JSON line. Extra fields (single-GPU runs):
   roofline      the dominant kernel (fused GroupNorm conv) in steady state with HIP events on
                 the UNet's stream, its PMC HBM traffic (profiles/, this commit), the conv tiles'
                 HBM GB/s, and the attention kernels' MFMA utilisation;
-  sweep         N in {32, 64, 256, 1024} on one GPU (north_star's N set; N = 32 is the 8-GPU
-                shard of N = 256), same path;
+  sweep         N in {32, 64, 128, 256, 1024} on one GPU (north_star's N set; N = 32 / 64 / 128 are
+                the 8- / 4- / 2-GPU shards of N = 256), same path;
   fp32          the reference-precision (parity mode) throughput at the headline N;
   legs          the other BASELINE configs per GPU shard: C3 CFG zero-order round (Arch C,
                 N_local = 32 -> 2N = 64 guided batch), C4 64x64 Arch A (N_local = 16), C5
@@ -70,7 +70,7 @@ def cpu_baseline(T: int, seconds: float = 12.0, check_seconds: float = 10.0):
 
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    torch.set_num_threads(cores)
+    torch.set_num_threads(cores)  # once, before any CPU op (the intra-op pool is sized here)
     a = ARCH_A
     sd = synthetic_state_dict(a, 0)
     fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
@@ -78,6 +78,7 @@ def cpu_baseline(T: int, seconds: float = 12.0, check_seconds: float = 10.0):
     def fwd_rate(b, window):
         x = torch.randn(b, 3, 32, 32)
         t = torch.full((b,), 500, dtype=torch.long)
+        fw(x, t)  # untimed: this batch's allocations (the caching allocator keeps them) and kernel choices
         n, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < window or n == 0:
             fw(x, t)
@@ -462,7 +463,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         # north_star N sweep on the same path (headline N is the main line)
         sweep = {}
-        for n, window in ((32, 1000), (64, 1000), (256, 1000), (1024, 100)):
+        for n, window in ((32, 1000), (64, 1000), (128, 1000), (256, 1000), (1024, 100)):
             if n == n_local:
                 continue
             progress(f"sweep N={n}")

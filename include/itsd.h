@@ -10,6 +10,8 @@
  *                                   Diffusion/Train.py:814-818)
  *   itsd_unet_forward            <- UNet.forward(x, t[, labels])   (Model.py:265,
  *                                   ModelCondition.py:206)
+ *   itsd_unet_representation     <- UNet.forward(..., return_representation=True)'s second
+ *                                   output, the pre-tail h (ModelCondition.py:206,225-235)
  *   itsd_set_schedule            <- GaussianDiffusionSampler.__init__ tables
  *                                   (Diffusion/Diffusion.py:51-65, DiffusionCondition.py:57-73)
  *   itsd_sampler_run             <- GaussianDiffusionSampler.forward loop
@@ -96,6 +98,11 @@ int itsd_unet_destroy(itsd_unet* u);
 int itsd_unet_forward(itsd_unet* u, const float* x, const int32_t* t, const int32_t* labels,
                       float* eps, int n, void* stream);
 
+/* repr[n,C,H,W] (NCHW fp32) = the pre-tail activation h of the LAST itsd_unet_forward on this handle
+ * (ModelCondition.py:225-235: last_representation = h before self.tail), C = ch * ch_mult[0];
+ * stream-ordered after that forward (same stream, or synchronised); n <= that forward's n. */
+int itsd_unet_representation(itsd_unet* u, float* repr, int n, void* stream);
+
 /* Host fp32 tables of length T: coeff1, coeff2 and sqrt(var) (the fp32 casts the
  * reference's extract() produces, Diffusion.py:9-16), plus the CFG weight w. */
 int itsd_set_schedule(itsd_unet* u, int T, const float* coeff1, const float* coeff2,
@@ -176,7 +183,7 @@ int itsd_set_option(const char* key, int value);
 int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value);
 
 /* Name of census kernel id `id` (itsd_profile_ops): the launch site's kernel expression,
- * e.g. "conv3x3_gn_pws_kernel<32>"; "" for 0 / unknown ids. */
+ * e.g. "conv3x3_gn_p4_kernel<32>"; "" for 0 / unknown ids. */
 const char* itsd_kernel_name(int id);
 
 const char* itsd_last_error(void);

@@ -37,7 +37,8 @@ def _needs(obj, deps):
 
 def build(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    # every file a .hip may include (headers and .inc fragments) is a dependency of every object
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))]
     headers.append(os.path.join(INCLUDE, "itsd.h"))
     jobs = []
     objs = []

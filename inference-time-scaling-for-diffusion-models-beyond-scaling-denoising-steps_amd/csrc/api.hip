@@ -52,6 +52,7 @@ bool tail_mfma_ok(int H, int W, int C);
 int g_io_mfma = 1;  // bf16 head / tail on MFMA (itsd_set_option "io_mfma", read at create)
 hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
                         hipStream_t);
+template <typename T> hipError_t launch_nhwc_to_nchw(const void*, float*, int, int, int, hipStream_t);
 }  // namespace itsd
 
 using namespace itsd;
@@ -109,7 +110,7 @@ struct Op {
   int ksize = 3, stride = 1, pad = 1, upsample = 0, zins = 0;
   int subpix = 0;  // upsample conv as 4 phase-wise 2x2 convs (conv.hip conv_pipe)
   size_t wt = 0, bias = 0;
-  size_t wfrag = SIZE_MAX;  // fragment-ordered copy of wt (fused GroupNorm convs, conv3x3_gn_reg_kernel)
+  size_t wfrag = SIZE_MAX;  // fragment-ordered copy of wt (fused GroupNorm convs: conv3x3_gn_p4 / p5_kernel)
   size_t wfrag16 = SIZE_MAX;  // the same for the 16x16x32 MFMA (conv3x3_gn_p4_kernel<.., true>)
   int Cout = 0, K = 0;
   int temb_col = -1;
@@ -152,6 +153,7 @@ struct itsd_unet {
   bool cfg = false;
   int H = 32, ch = 128, tdim = 512, sumC = 0;
   int nb_max = 0;  // capacity in images (CFG: 2 * max_batch)
+  int last_forward_n = 0;  // batch of the last itsd_unet_forward (itsd_unet_representation reads its tail input)
 
   char* wdev = nullptr;
   char* ws = nullptr;
@@ -190,7 +192,6 @@ struct itsd_unet {
   void* zero_page = nullptr;  // 256 KiB of zeros (conv DMA source for padding, conv.hip zero_of_block)
   float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
   int* tickets = nullptr;      // in-launch split-K counters (conv3x3_gn_p5_kernel), zero between launches
-  static constexpr long long kTicketCap = 16384;
   static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
 
   hipStream_t stream = nullptr;
@@ -1110,33 +1111,28 @@ int itsd_set_option(const char* key, int value) {
     // conv) s_setprio 1 for waves 4-7 (results unchanged), 1024 / 2048 (wide
     // fused conv) every lane reads the same B / A fragment row (LDS broadcast). (Never skip an issued load's wait: an
     // in-flight load landing in a reused register faults.)
-    // 4096 | (mask << 13): compile-time ablations of conv3x3_gn_reg_kernel<32> (conv.hip)
-    // (1 << 20) / (1 << 21): s_setprio 1 / 2 for the halo waves of the ws / pws fused GroupNorm convs
-    itsd::g_conv_dbg = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13) | (3 << 20));
+    // 4096 | (mask << 13): compile-time ablations of conv3x3_gn_p4_kernel<32> (conv.hip, diagnostic builds)
+    // (1 << 20) / (1 << 21): s_setprio 1 / 2 for the halo waves of the fused GroupNorm conv
+    const int v = value & (1 | 2 | 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 | (127 << 13) | (3 << 20));
 #ifndef ITSD_DIAG
-    if (itsd::g_conv_dbg & 4096) {
-      itsd::g_conv_dbg = 0;
-      return fail(ITSD_ERR_INVALID, "conv_dbg 4096 (compile-time ablations): diagnostic builds only (tools/build_diag.sh)");
-    }
+    // validated before it is stored: a refused call leaves the previous setting in place
+    if (v & 4096) return fail(ITSD_ERR_INVALID, "conv_dbg 4096 (compile-time ablations): diagnostic builds only (tools/build_diag.sh)");
 #endif
+    itsd::g_conv_dbg = v;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "gn_wide") || !std::strcmp(key, "conv_wide")) {
-    // 256-pixel conv tiles (gn_wide: the persistent conv3x3_gn_p4_kernel; conv_wide: conv_pipe_wide,
-    // diagnostic builds only): 0 off, 1 auto, 2 whenever eligible
-    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, std::string(key) + " in [0,2]");
-#ifndef ITSD_DIAG
-    if (key[0] == 'c' && value) return fail(ITSD_ERR_INVALID, "conv_wide: diagnostic builds only (tools/build_diag.sh)");
-#endif
-    (key[0] == 'g' ? itsd::g_gn_wide : itsd::g_conv_wide) = value;
+  if (!std::strcmp(key, "gn_wide")) {  // the persistent 256-pixel fused conv: 0 off, 1 auto, 2 whenever eligible
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "gn_wide in [0,2]");
+    itsd::g_gn_wide = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "gn_reg")) {
-    // 4: conv3x3_gn_p4_kernel (shipped); 0-3: the superseded 256-pixel kernels, diagnostic builds only
-    if (value < 0 || value > 4) return fail(ITSD_ERR_INVALID, "gn_reg in [0,4]");
-#ifndef ITSD_DIAG
-    if (value != 4) return fail(ITSD_ERR_INVALID, "gn_reg 0-3 (superseded 256-pixel kernels): diagnostic builds only");
-#endif
+  if (!std::strcmp(key, "conv_wide")) {  // round 3's 256-pixel plain conv (deleted): only 0 is accepted
+    if (value != 0) return fail(ITSD_ERR_INVALID, "conv_wide: the 256-pixel plain conv was removed (only 0)");
+    itsd::g_conv_wide = 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "gn_reg")) {  // 4: conv3x3_gn_p4_kernel; the superseded generations 0-3 were removed
+    if (value != 4) return fail(ITSD_ERR_INVALID, "gn_reg: only 4 (conv3x3_gn_p4_kernel) exists");
     itsd::g_gn_reg = value;
     return ITSD_OK;
   }
@@ -1158,7 +1154,7 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_m16 = value ? 1 : 0;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "p4_w")) {  // levels gn_reg = 4 applies to (bit 0 W = 8, 1 W = 16, 2 W = 32); others pws
+  if (!std::strcmp(key, "p4_w")) {  // levels conv3x3_gn_p4_kernel takes (bit 0 W = 8, 1 W = 16, 2 W = 32); others p5 / 128-px
     if (value < 0 || value > 7) return fail(ITSD_ERR_INVALID, "p4_w in [0,7]");
     itsd::g_p4_w = value;
     return ITSD_OK;
@@ -1183,7 +1179,7 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p5_split = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p5_kernel: 0 off, 1 on
+  if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p4 / p5_kernel: 0 off, 1 on
     itsd::g_gn_fold = value ? 1 : 0;
     return ITSD_OK;
   }
@@ -1249,8 +1245,8 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipMalloc(&u->zero_page, 64 * 4096 + 1024));
   HIPCHK(hipMemset(u->zero_page, 0, 64 * 4096 + 1024));
   HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
-  HIPCHK(hipMalloc(&u->tickets, itsd_unet::kTicketCap * 4));
-  HIPCHK(hipMemset(u->tickets, 0, itsd_unet::kTicketCap * 4));
+  HIPCHK(hipMalloc(&u->tickets, itsd::kTicketCap * 4));
+  HIPCHK(hipMemset(u->tickets, 0, itsd::kTicketCap * 4));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -1294,6 +1290,25 @@ int itsd_unet_forward(itsd_unet* u, const float* x, const int32_t* t, const int3
   c.labels = labels; c.label_mod = n; c.uncond_from = -1;
   c.tail.n = n; c.tail.cfg = 0; c.tail.step_mode = 0; c.tail.eps_out = eps;
   CHK(run_program(u, c, s));
+  u->last_forward_n = n;
+  HIPCHK(hipEventRecord(u->ev_out, s));
+  HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
+  return ITSD_OK;
+}
+
+int itsd_unet_representation(itsd_unet* u, float* repr, int n, void* stream) {
+  if (!u || !repr) return fail(ITSD_ERR_INVALID, "null argument");
+  if (u->last_forward_n == 0) return fail(ITSD_ERR_INVALID, "itsd_unet_representation: no itsd_unet_forward on this handle yet");
+  if (n < 1 || n > u->last_forward_n)
+    return fail(ITSD_ERR_INVALID, "itsd_unet_representation: n outside [1, last forward's batch]");
+  HIPCHK(hipSetDevice(u->device));
+  const Act& A = u->acts[u->tail_in];
+  hipStream_t cs = (hipStream_t)stream;
+  hipStream_t s = u->stream;
+  HIPCHK(hipEventRecord(u->ev_in, cs));
+  HIPCHK(hipStreamWaitEvent(s, u->ev_in, 0));
+  HIPCHK(u->bf16 ? launch_nhwc_to_nchw<bf16_t>(u->ap(u->tail_in), repr, n, A.H * A.W, A.C, s)
+                 : launch_nhwc_to_nchw<float>(u->ap(u->tail_in), repr, n, A.H * A.W, A.C, s));
   HIPCHK(hipEventRecord(u->ev_out, s));
   HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
   return ITSD_OK;

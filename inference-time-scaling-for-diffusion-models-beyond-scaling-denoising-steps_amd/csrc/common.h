@@ -40,6 +40,11 @@ int kernel_id(const char* name);
 
 typedef uint16_t bf16_t;  // storage type for bf16 activations / weights
 
+// In-launch split-K tickets per UNet handle: the hipMalloc'd counter array (api.hip itsd_unet::tickets)
+// and every launch-side bound on ticket indices (conv.hip: conv_pipe / conv_small tile, p5 tile * 4 + wave)
+// use this one constant.
+constexpr long long kTicketCap = 16384;
+
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;

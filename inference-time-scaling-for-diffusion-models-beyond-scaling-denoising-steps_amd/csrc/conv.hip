@@ -31,7 +31,6 @@
 namespace itsd {
 
 constexpr int CONV_BM = 128;  // couts per block
-constexpr long long kTicketCap = 16384;  // split-K tickets per UNet handle (itsd_unet::tickets)
 constexpr int CONV_BN = 128;  // pixels per block
 constexpr int ROWB = 128;     // bytes per LDS row
 constexpr int TILEB = 128 * ROWB;
@@ -44,21 +43,19 @@ int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
-int g_gn_reg = 4;        // fused GroupNorm conv with the weights streamed into registers where the
-                         // 256-pixel tile applies: 0 off, 1 conv3x3_gn_reg_kernel, 2 warp-specialized
-                         // conv3x3_gn_ws_kernel (halo waves), 3 persistent conv3x3_gn_pws_kernel,
-                         // 4 persistent with one MFMA wave per SIMD (conv3x3_gn_p4_kernel)
+int g_gn_reg = 4;        // the 256-pixel fused GroupNorm conv: 4 = conv3x3_gn_p4_kernel (the only shipped
+                         // generation; the superseded 0-3 were deleted in round 4)
 int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel chunk, 0 tap-major (default: 1 measured 2-3 % slower)
-int g_p4_w = 7;
-int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)         // levels conv3x3_gn_p4_kernel takes under gn_reg = 4: bit 0 W = 8, 1 W = 16, 2 W = 32
+int g_p4_w = 7;          // levels conv3x3_gn_p4_kernel takes: bit 0 W = 8, 1 W = 16, 2 W = 32
+int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
-int g_conv_wide = 0;     // 256-pixel plain conv (conv_pipe_wide): 0 off (default: measured slower than
-                         // conv_pipe / conv_small at N = 256), 1 auto, 2 whenever eligible
+int g_conv_wide = 0;     // (round 3's 256-pixel plain conv, measured slower than conv_pipe / conv_small and
+                         // deleted in round 4: only 0 is accepted)
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -1214,12 +1211,6 @@ template <> struct GnpCfg<32> { static constexpr int NSEG = 1, ITEMS = 11, RES =
 template <> struct GnpCfg<16> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 0; };  // LDS: residual from HBM
 
-#ifdef ITSD_DIAG
-// Diagnostic builds only (hipcc -DITSD_DIAG, tools/build_diag.sh): the superseded 256-pixel fused-conv
-// generations (LDS weight ring, weights in registers, warp-specialised, two MFMA waves per SIMD) and the
-// 256-pixel plain conv, kept as A/B references for measurements. Never in the shipped library.
-#include "conv_diag.inc"
-#endif
 
 // ---------------------------------------------------------------------------- persistent, one MFMA wave per SIMD
 // conv3x3_gn_pws_kernel's ablations (profiles/r02_pws_ablations.txt): without the B-fragment LDS
@@ -2880,38 +2871,6 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout) {
   return segs && (g_gn_wide == 2 || blocks >= 192) ? segs : 0;
 }
 
-#ifdef ITSD_DIAG
-// conv_pipe_wide for plain bf16 convs in whole 64-channel K-chunks whose 256-pixel tiles hold
-// whole images or whole GroupNorm statistics slots. Auto: at least 12 K-stages (short-K 1x1s
-// stay on the 2-blocks-per-CU conv_pipe) and ~one block per CU (split K below that). Returns
-// true when it launched (*err set).
-static bool conv_wide_launch(const ConvArgs& a, hipStream_t s, hipError_t* err) {
-  if (!g_conv_wide) return false;
-  const int HWo = a.Hout * a.Wout, Cin = a.C1 + a.C2;
-  if (!a.zero || a.subpix || a.upsample || a.zins || a.gn_coef || Cin % 64 || a.C1 % 64 || a.Cout % 8 ||
-      a.K != a.ksize * a.ksize * Cin || a.ksize > 5 || (HWo % GNW_BN && GNW_BN % HWo) || (HWo % 128 && 128 % HWo) ||
-      (a.vt_out && HWo % 8))
-    return false;
-  dim3 grid((a.M + GNW_BN - 1) / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
-  const int blocks = (int)(grid.x * grid.y), nK = a.ksize * a.ksize * (Cin / 64);
-  if (g_conv_wide != 2 && nK < 12) return false;
-  int S = 1;
-  if (blocks < 192 && a.splitk_ws && g_splitk) {  // under-filled: about one block per CU, >= 8 stages a slice
-    S = std::min((256 + blocks - 1) / blocks, nK / 8);
-    while (S > 1 && (long long)blocks * S * 32768 > a.splitk_cap) --S;
-    if (S < 1) S = 1;
-  }
-  if (g_conv_wide != 2 && blocks * S < 192) return false;
-  grid.z = S;
-  ITSD_LAUNCH(conv_pipe_wide, grid, dim3(512), 0, s, a);
-  *err = hipGetLastError();
-  if (*err == hipSuccess && S > 1) {
-    ITSD_LAUNCH(splitk_wide_epilogue_kernel, dim3(grid.x, grid.y), dim3(512), 0, s, a, S);
-    *err = hipGetLastError();
-  }
-  return true;
-}
-#endif
 
 // conv3x3_gn_p5_kernel: levels whose 128-pixel tiles hold whole images
 bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 || W == 32 || W == 64); }
@@ -2996,33 +2955,6 @@ static hipError_t launch_p4_ablation(const ConvArgs& a, dim3 gp, hipStream_t s) 
   return hipGetLastError();
 }
 
-// Diagnostic builds: the superseded 256-pixel fused convs (gn_reg = 3 pws, 2 ws, 1 reg, 0 wide)
-static bool launch_gn_wide_diag(const ConvArgs& a, int segs, hipStream_t s, hipError_t* err) {
-  const dim3 gw(a.M / GNW_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
-  const bool sq = a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
-  if (g_gn_reg >= 3 && sq) {
-    const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
-    const dim3 gp(std::min(tiles, g_num_cus));
-    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_pws_kernel<32>, gp, dim3(768), 0, s, a);
-    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_pws_kernel<16>, gp, dim3(768), 0, s, a);
-    else ITSD_LAUNCH(conv3x3_gn_pws_kernel<8>, gp, dim3(768), 0, s, a);
-  } else if (g_gn_reg == 2 && sq && a.C1 + a.C2 <= GNS_MAXC) {
-    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_ws_kernel<32>, gw, dim3(768), 0, s, a);
-    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_ws_kernel<16>, gw, dim3(768), 0, s, a);
-    else ITSD_LAUNCH(conv3x3_gn_ws_kernel<8>, gw, dim3(768), 0, s, a);
-  } else if (g_gn_reg == 1 && sq) {
-    if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_reg_kernel<32>, gw, dim3(512), 0, s, a);
-    else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_reg_kernel<16>, gw, dim3(512), 0, s, a);
-    else ITSD_LAUNCH(conv3x3_gn_reg_kernel<8>, gw, dim3(512), 0, s, a);
-  } else if (g_gn_reg == 0) {
-    if (segs == 1) ITSD_LAUNCH(conv3x3_gn_wide_kernel<1>, gw, dim3(512), 0, s, a);
-    else ITSD_LAUNCH(conv3x3_gn_wide_kernel<4>, gw, dim3(512), 0, s, a);
-  } else {
-    return false;
-  }
-  *err = hipGetLastError();
-  return true;
-}
 #endif
 
 template <typename T>
@@ -3046,10 +2978,6 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }
-#ifdef ITSD_DIAG
-        hipError_t de;
-        if (launch_gn_wide_diag(a, segs, s, &de)) return de;
-#endif
       }
       dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
       const int THs = std::min(a.Hout, 128 / a.Wout), segs = 128 / (THs * a.Wout);
@@ -3060,12 +2988,6 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   }
   constexpr int BK = 8 * (16 / (int)sizeof(T));
   dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
-#ifdef ITSD_DIAG
-  if constexpr (sizeof(T) == 2) {
-    hipError_t we;
-    if (conv_wide_launch(a, s, &we)) return we;
-  }
-#endif
   if constexpr (sizeof(T) == 2) {
     if (conv_p4_plain_selected(a)) {
       const dim3 gp(std::min((a.M / GNW_BN) * (a.Cout / CONV_BM), g_num_cus));

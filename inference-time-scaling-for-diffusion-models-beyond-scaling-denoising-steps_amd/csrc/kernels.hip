@@ -329,8 +329,10 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(AttnArgs a) {
 //   5. out = x + O Wp^T + bp, one bf16 rounding, 16-B stores (permlane32 swap), and the consumer
 //      GroupNorm statistics of out (one slot per image) by lane butterflies.
 // Roundings as the unfused path: hn, q / k / v, P and O in bf16, fp32 accumulation.
-// 4 waves; weights (fragment-packed [Cout/32][K/16][64][8] bf16) stream from L2 into VGPRs with a
-// 4-k-step prefetch; one block per image.
+// 8 waves (512 threads, __launch_bounds__(512, 1)): the weight-streaming phases give each wave whole
+// 32-channel blocks (V / proj: blocks w, w + 8; q|k: Q on waves 0-3, K on 4-7), the score / softmax / PV
+// phases split queries and channel blocks over the waves; weights (fragment-packed [Cout/32][K/16][64][8]
+// bf16) stream from L2 into VGPRs with an 8-k-step prefetch; one block per image.
 
 #ifdef ITSD_STAMPS
 // Diagnostic build only: attn_block_kernel's phase timeline (s_memrealtime), [block % 1024][wave][slot]
@@ -1562,6 +1564,33 @@ hipError_t launch_noise(float* out, const float* pivot, int n_cand, long long pe
                      scale, seed, stream_id, cand_offset * per_cand);
   return hipGetLastError();
 }
+
+// ============================================================================ representation
+// The pre-tail activation (NHWC, bf16 or fp32) of image img -> NCHW fp32 (ModelCondition.py:225-235's
+// last_representation): 64 pixels x 64 channels per block through LDS, coalesced on both sides.
+template <typename T>
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const T* in, float* out, int HW, int C) {
+  __shared__ float tile[64][65];
+  const int img = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, tid = threadIdx.x;
+  const T* src = in + (size_t)img * HW * C;
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int p = i >> 6, c = i & 63;
+    tile[p][c] = (p0 + p < HW && c0 + c < C) ? Elem<T>::tof(src[(size_t)(p0 + p) * C + c0 + c]) : 0.f;
+  }
+  __syncthreads();
+  float* dst = out + (size_t)img * C * HW;
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int c = i >> 6, p = i & 63;
+    if (p0 + p < HW && c0 + c < C) dst[(size_t)(c0 + c) * HW + p0 + p] = tile[p][c];
+  }
+}
+template <typename T>
+hipError_t launch_nhwc_to_nchw(const void* in, float* out, int n, int HW, int C, hipStream_t s) {
+  ITSD_LAUNCH(nhwc_to_nchw_kernel<T>, dim3((HW + 63) / 64, (C + 63) / 64, n), dim3(256), 0, s, (const T*)in, out, HW, C);
+  return hipGetLastError();
+}
+template hipError_t launch_nhwc_to_nchw<float>(const void*, float*, int, int, int, hipStream_t);
+template hipError_t launch_nhwc_to_nchw<bf16_t>(const void*, float*, int, int, int, hipStream_t);
 
 // ============================================================================ small utilities
 __global__ void set_int_kernel(int* p, int v) { *p = v; }

@@ -45,6 +45,7 @@ class GaussianDiffusionSampler:
         self.coeff2 = self.sched.coeff2
         self.posterior_var = self.sched.posterior_var
         self._sched_args = (self.sched.coeff1_f32, self.sched.coeff2_f32, self.sched.sqrt_var_f32, self.w)
+        self.last_seed = None  # Philox key of the last run (set by run)
 
     def to(self, *args, **kwargs):
         if args or "device" in kwargs:
@@ -86,6 +87,7 @@ class GaussianDiffusionSampler:
             clip = t_end == 0
         if seed is None and noise is None:
             seed = _draw_seed()
+        self.last_seed = seed  # the Philox key of this run (None with injected noise)
         if noise is not None:
             noise = noise.to(x.device, torch.float32).contiguous()
             if noise.shape[0] < t_begin + 1 or noise[0].numel() != x.numel():

@@ -241,16 +241,24 @@ def _device(cfg: Dict[str, Any]) -> torch.device:
         ids = [int(ids)]
     local = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+
+    def checked(i: int, key: str) -> torch.device:
+        n = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
+        if n and not 0 <= i < n:
+            raise ValueError(f"config key '{key}' selects cuda:{i} but this process sees {n} GPU(s)"
+                             + (f" (LOCAL_RANK {local})" if "LOCAL_RANK" in os.environ else ""))
+        return torch.device("cuda", i)
+
     if ids:
         if world > 1 and local >= len(ids):
             raise ValueError(f"device_ids {list(ids)} has no entry for LOCAL_RANK {local}")
-        return torch.device("cuda", int(ids[local if world > 1 else 0]))
+        return checked(int(ids[local if world > 1 else 0]), "device_ids")
     dev = torch.device(spec.split(",")[0])
     if world > 1:  # one GPU per rank: the configured index is the first rank's
-        return torch.device("cuda", (dev.index or 0) + local)
+        return checked((dev.index or 0) + local, "device")
     if dev.index is None:
-        dev = torch.device("cuda", local if "LOCAL_RANK" in os.environ else torch.cuda.current_device())
-    return dev
+        return checked(local if "LOCAL_RANK" in os.environ else torch.cuda.current_device(), "device")
+    return checked(dev.index, "device")
 
 
 def detect_checkpoint_T(state_dict: Dict[str, torch.Tensor]) -> Optional[int]:
@@ -478,7 +486,7 @@ def eval(cfg: Dict[str, Any]) -> Dict[str, Any]:  # noqa: A001 (reference name)
             save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]),
                        nrow=cfg["nrow"])
             save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
-        res = {"noisy": noisy, "sampled": imgs}
+        res = {"noisy": noisy, "sampled": imgs, "sampler_seed": sampler.last_seed}
         res["search"] = _search(cfg, sampler, img_size, None)
     return res
 
@@ -503,7 +511,7 @@ def eval_condition(cfg: Dict[str, Any]) -> Dict[str, Any]:
             save_image(torch.clamp(noisy * 0.5 + 0.5, 0, 1), os.path.join(d, cfg["sampledNoisyImgName"]),
                        nrow=cfg["nrow"])
             save_image(imgs, os.path.join(d, cfg["sampledImgName"]), nrow=cfg["nrow"])
-        res = {"noisy": noisy, "sampled": imgs, "labels": labels}
+        res = {"noisy": noisy, "sampled": imgs, "labels": labels, "sampler_seed": sampler.last_seed}
         res["search"] = _search(cfg, sampler, img, labels)
     return res
 

@@ -150,9 +150,9 @@ class CondUNet(_NativeModule):
         self.dropout = dropout
         self._init_common(arch, precision, weights, seed, device)
 
-    def forward(self, x: torch.Tensor, t, labels, return_representation: bool = False) -> torch.Tensor:
-        if return_representation:
-            raise NotImplementedError("return_representation (ModelCondition.py:225-235) is a training-side output")
+    def forward(self, x: torch.Tensor, t, labels, return_representation: bool = False):
+        """``ModelCondition.py:206-235``: eps, or (eps, h) with h the pre-tail activation
+        (``last_representation``, NCHW fp32 [B, ch * ch_mult[0], H, W]) when return_representation."""
         x, t = self._prep(x, t)
         lab = labels.flatten().to(self.device, torch.int32).contiguous()
         if int(lab.min()) < 0 or int(lab.max()) > self.arch.num_labels:
@@ -160,7 +160,11 @@ class CondUNet(_NativeModule):
         if int(t.max()) >= self.arch.T or int(t.min()) < 0:
             raise IndexError("t out of range for the time-embedding table (ModelCondition.py:38)")
         eps = torch.empty_like(x)
-        self.native(x.shape[0]).forward(x, t, lab, eps)
+        nat = self.native(x.shape[0])
+        nat.forward(x, t, lab, eps)
+        if return_representation:
+            a = self.arch
+            return eps, nat.representation(x.shape[0], a.ch * a.ch_mult[0], a.img_size, x.device)
         return eps
 
     __call__ = forward

@@ -50,6 +50,7 @@ _SIGS = {
     "itsd_unet_destroy": [ctypes.c_void_p],
     "itsd_unet_forward": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                           ctypes.c_int, ctypes.c_void_p],
+    "itsd_unet_representation": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
     "itsd_set_schedule": [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                           ctypes.c_float],
     "itsd_sampler_run": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -163,6 +164,12 @@ class NativeUNet:
     def forward(self, x: torch.Tensor, t: torch.Tensor, labels: Optional[torch.Tensor], eps: torch.Tensor) -> None:
         check(lib().itsd_unet_forward(self.h, x.data_ptr(), t.data_ptr(), _ptr(labels), eps.data_ptr(),
                                       x.shape[0], stream_ptr(x.device)))
+
+    def representation(self, n: int, channels: int, hw: int, device) -> torch.Tensor:
+        """The pre-tail activation of the last forward as NCHW fp32 [n, channels, hw, hw]."""
+        out = torch.empty(n, channels, hw, hw, dtype=torch.float32, device=device)
+        check(lib().itsd_unet_representation(self.h, out.data_ptr(), int(n), stream_ptr(out.device)))
+        return out
 
     def set_schedule(self, coeff1: torch.Tensor, coeff2: torch.Tensor, sqrt_var: torch.Tensor, w: float = 0.0):
         c1 = coeff1.detach().cpu().float().contiguous()

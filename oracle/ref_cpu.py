@@ -120,8 +120,10 @@ def _mlp_from_table(sd: SD, p: str, idx: Tensor) -> Tensor:
 
 
 def unet_forward(sd: SD, x: Tensor, t: Tensor, ch: int, ch_mult: Sequence[int], attn: Sequence[int],
-                 num_res_blocks: int, labels: Optional[Tensor] = None, cfg: bool = False) -> Tensor:
-    """``Model.py:265-285`` (DDPM) / ``ModelCondition.py:206-235`` (CFG)."""
+                 num_res_blocks: int, labels: Optional[Tensor] = None, cfg: bool = False,
+                 return_representation: bool = False):
+    """``Model.py:265-285`` (DDPM) / ``ModelCondition.py:206-235`` (CFG; with
+    ``return_representation`` it returns (eps, h) with h the pre-tail activation, ``:225-235``)."""
     if cfg:
         temb = _mlp_from_table(sd, "time_embedding.timembedding", t)
         cemb = _mlp_from_table(sd, "cond_embedding.condEmbedding", labels)
@@ -153,10 +155,11 @@ def unet_forward(sd: SD, x: Tensor, t: Tensor, ch: int, ch_mult: Sequence[int], 
         else:  # UpSample Model.py:121-126
             h = F.interpolate(h, scale_factor=2, mode="nearest")
             h = F.conv2d(h, sd[p + ".main.weight"], sd[p + ".main.bias"], padding=1)
+    rep = h  # ModelCondition.py:225 last_representation
     h = F.group_norm(h, 32, sd["tail.0.weight"], sd["tail.0.bias"], 1e-5)
     h = F.conv2d(_silu(h), sd["tail.2.weight"], sd["tail.2.bias"], padding=1)
     assert not hs
-    return h
+    return (h, rep) if return_representation else h
 
 
 # --------------------------------------------------------------------------- sampler

@@ -57,8 +57,8 @@ int main() {
   expect("set_option gn_wide=7", itsd_set_option("gn_wide", 7), ITSD_ERR_INVALID);
   expect("set_option gn_reg=5", itsd_set_option("gn_reg", 5), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_OK);
-  expect("set_option gn_reg=3 (diagnostic builds only)", itsd_set_option("gn_reg", 3), ITSD_ERR_INVALID);
-  expect("set_option conv_wide=1 (diagnostic builds only)", itsd_set_option("conv_wide", 1), ITSD_ERR_INVALID);
+  expect("set_option gn_reg=3 (removed)", itsd_set_option("gn_reg", 3), ITSD_ERR_INVALID);
+  expect("set_option conv_wide=1 (removed)", itsd_set_option("conv_wide", 1), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
   expect("set_option p4_w=8", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
@@ -123,6 +123,7 @@ int main() {
   int ki[4] = {0};
   int64_t q = 0;
   expect("forward null handle", itsd_unet_forward(nullptr, f, ti, nullptr, f, 1, nullptr), ITSD_ERR_INVALID);
+  expect("representation null handle", itsd_unet_representation(nullptr, f, 1, nullptr), ITSD_ERR_INVALID);
   expect("set_schedule null handle", itsd_set_schedule(nullptr, 4, f, f, f, 0.f), ITSD_ERR_INVALID);
   expect("sampler_run null handle", itsd_sampler_run(nullptr, f, nullptr, 1, 3, 0, 1, 0, nullptr, 0, nullptr),
          ITSD_ERR_INVALID);

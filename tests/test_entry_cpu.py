@@ -108,3 +108,33 @@ def test_train_state_and_cpu_device_rejected():
         E.run({"state": "train"})
     with pytest.raises(ValueError):
         E._device({"device": "cpu"})
+
+
+def test_png_grid_geometry_matches_reference_images(tmp_path):
+    """The grids save_image writes have the geometry of the reference's own PNGs
+    (SampledImgs/*.png, tests/golden/png_grids.json by tools/gen_golden_png.py): 8 x 8 and 8 x 10
+    grids of 32-px images -> 274 x 274 and 274 x 342, 8-bit RGB (PNG colour type 2), and the
+    2-pixel separators are 0 as in the reference files (padding_max 0 there). Pixel values are
+    unpinned: the reference ships no seeds or weights for its images."""
+    import json
+    import struct
+
+    from PIL import Image
+
+    with open(os.path.join(ROOT, "tests", "golden", "png_grids.json")) as fh:
+        gold = json.load(fh)
+    for name, g in gold.items():
+        n = g["rows"] * g["cols"]
+        x = torch.rand(n, 3, 32, 32) * 0.8 + 0.1  # strictly inside (0, 1): no pixel is 0
+        p = str(tmp_path / name)
+        E.save_image(x, p, nrow=8)
+        with open(p, "rb") as fh:
+            head = fh.read(33)
+        w, h = struct.unpack(">II", head[16:24])
+        assert (w, h, head[24], head[25]) == (g["width"], g["height"], g["bit_depth"], g["color_type"]), name
+        arr = np.asarray(Image.open(p))
+        pad = [r for r in range(h) if r % 34 in (0, 1)]
+        padc = [c for c in range(w) if c % 34 in (0, 1)]
+        assert max(arr[pad].max(), arr[:, padc].max()) == g["padding_max"] == 0
+        inner = np.delete(np.delete(arr, pad, axis=0), padc, axis=1)
+        assert inner.min() > 0  # every non-separator pixel belongs to an image

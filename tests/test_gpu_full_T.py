@@ -1,0 +1,128 @@
+"""Full-length sampled images and scores against the oracle ("Pin full-length sampled
+images and scores"; north_star: "sampled images match the reference PyTorch CPU path on fixed seeds
+within a stated fp32 tolerance").
+
+One module fixture runs, on the GPU:
+  C1   Main.py's eval (config/config.yaml keys through itsd.entry, ``Diffusion/Train.py:808-843``):
+       Arch A, T = 1000, fp32 (the reference's precision), synthetic weights, batch_size 1 and 2 --
+       the whole ancestral loop ``Diffusion/Diffusion.py:84-102`` in Philox mode;
+  C2   one bf16 random-search round of N = 256 Philox candidates at T = 1000 (the bench's round,
+       ``search/search_algorithm.py:54-83``) scored by the OracleVerifier (``search/verifier.py:45-66``),
+and then the oracle's full 1000-step loop (``oracle.ref_cpu.p_sample_loop``, fp32 CPU) over the two
+C1 runs' 3 images and 3 of the 256 candidates (indices 0, 129, 255) in ONE batched loop, each image
+fed its own counter-based noise (``R.philox_normal``: the seed the run used, the image's global
+element offset), so every comparison is one image's whole trajectory.
+
+Tolerances (measured values are printed):
+  C1 fp32 x0 (the saved image x0 * 0.5 + 0.5)      max|d| <= FULL_T_FP32_MAXABS
+  C2 bf16 x0 vs the fp32 oracle                    per-image rel-L2 <= FULL_T_BF16_REL_L2
+  C2 per-candidate Oracle-verifier score           |d| <= FULL_T_BF16_SCORE (the quantity the
+                                                   search prunes on)
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+from itsd import entry as E
+from itsd.arch import ARCH_A
+from itsd.diffusion import GaussianDiffusionSampler
+from itsd.model import UNet
+from itsd.search import SearchEngine
+from itsd.verifier import OracleVerifier
+from itsd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+FULL_T_FP32_MAXABS = 2e-3
+FULL_T_BF16_REL_L2 = 5e-2
+FULL_T_BF16_SCORE = 5e-3
+
+T = 1000
+PER = 3 * 32 * 32
+STREAM_XT = 0xF0000000  # itsd.search._STREAM_XT: candidate x_T of round 0
+CANDS = (0, 129, 255)
+ENGINE_SEED = 21
+
+
+def _rel_l2(a, b):
+    return (torch.linalg.norm((a - b).flatten()) / torch.linalg.norm(b.flatten())).item()
+
+
+@pytest.fixture(scope="module")
+def full_T(tmp_path_factory):
+    out = {}
+    # ---- C1: Main.py eval, batch_size 1 and 2 (fp32, T = 1000, Philox seed drawn by the sampler)
+    c1 = []
+    for bs, seed in ((1, 7), (2, 8)):
+        d = tmp_path_factory.mktemp(f"c1_bs{bs}")
+        cfg = E.load_config(None, ["weights=random", f"batch_size={bs}", "inference_T=1000", f"sampled_dir={d}",
+                                   f"seed={seed}", "nrow=8", "img_size=32"])
+        res = E.run(cfg)
+        assert res["sampler_seed"] is not None
+        c1.append({"x_T": res["noisy"].cpu(), "sampled": res["sampled"].cpu(), "seed": int(res["sampler_seed"])})
+        torch.cuda.empty_cache()
+    out["c1"] = c1
+    # ---- C2: a bf16 N = 256 Philox round (the bench's round protocol)
+    a = ARCH_A
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
+    net.load_state_dict(synthetic_state_dict(a, 0))
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
+    eng = SearchEngine(smp, OracleVerifier(), seed=ENGINE_SEED)
+    r = eng.run_round(0, 256, (1, 3, 32, 32))
+    run_seed = (ENGINE_SEED * 1000003 + 0) & ((1 << 62) - 1)  # SearchEngine.run_round's sampler key
+    out["c2"] = {"x0": r.local_images.cpu(), "scores": r.scores.clone(), "run_seed": run_seed}
+    del eng, smp, net
+    torch.cuda.empty_cache()
+    # ---- the oracle: one batched fp32 loop over the 6 images, each with its own noise stream
+    x_T, streams = [], []  # streams[i] = (seed, first global element of image i)
+    for run in c1:
+        for j in range(run["x_T"].shape[0]):
+            x_T.append(run["x_T"][j])
+            streams.append((run["seed"], j * PER))
+    for i in CANDS:
+        x_T.append(R.philox_normal(ENGINE_SEED, STREAM_XT, np.arange(i * PER, (i + 1) * PER)).reshape(3, 32, 32))
+        streams.append((run_seed, i * PER))
+    x_T = torch.stack(x_T)
+
+    def noise(step, xx):
+        return torch.stack([R.philox_normal(s, step, np.arange(o, o + PER)).reshape(3, 32, 32) for s, o in streams])
+
+    sd = synthetic_state_dict(a, 0)
+    fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
+    with torch.no_grad():
+        out["oracle_x0"] = R.p_sample_loop(fw, x_T, R.schedule(1e-4, 0.02, T), noise)
+    out["oracle_x_T"] = x_T
+    return out
+
+
+def test_C1_main_eval_T1000_fp32_vs_oracle(full_T):
+    """Main.py's eval end to end at the reference's precision: the saved image (x0 * 0.5 + 0.5) of
+    batch_size 1 and 2 against the oracle's full 1000-step loop on the same x_T and noise."""
+    ref = full_T["oracle_x0"] * 0.5 + 0.5
+    k = 0
+    for run in full_T["c1"]:
+        n = run["sampled"].shape[0]
+        d = (run["sampled"] - ref[k:k + n]).abs().max().item()
+        rel = _rel_l2(run["sampled"] * 2 - 1, full_T["oracle_x0"][k:k + n])
+        print(f"C1 batch {n}: full T=1000 fp32 x0 max|d| = {d:.3e} (rel-L2 of x0 {rel:.3e})")
+        assert d <= FULL_T_FP32_MAXABS
+        k += n
+
+
+def test_C2_bf16_round_T1000_candidates_and_scores_vs_oracle(full_T):
+    """Three candidates of one bf16 N = 256 round: the denoised x0 (rel-L2) and the OracleVerifier
+    score the search prunes on, against the fp32 oracle's full loop and R.oracle_score."""
+    c2 = full_T["c2"]
+    for k, i in enumerate(CANDS):
+        # the round's x_T is the Philox generator's (itsd_noise == R.philox_normal is pinned by
+        # test_gpu_search.test_philox_noise_kernel_matches_oracle), so the oracle started from it
+        ref = full_T["oracle_x0"][3 + k]
+        got = c2["x0"][i]
+        rel = _rel_l2(got, ref)
+        s_ref = R.oracle_score(ref.unsqueeze(0))
+        ds = abs(float(c2["scores"][i]) - s_ref)
+        print(f"C2 bf16 candidate {i}: x0 rel-L2 {rel:.3e}, max|d| {(got - ref).abs().max().item():.3e}; "
+              f"score {float(c2['scores'][i]):.6f} vs oracle {s_ref:.6f} (|d| {ds:.2e})")
+        assert rel <= FULL_T_BF16_REL_L2
+        assert ds <= FULL_T_BF16_SCORE

@@ -425,3 +425,52 @@ def test_forward_bf16_full_batch_vs_oracle_subset():
         ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
     for k, i in enumerate(idx.tolist()):
         assert _rel_l2(eps[i], ref[k]) < REL_L2_BF16, (i, _rel_l2(eps[i], ref[k]))
+
+
+# ----------------------------------------------------------------------------- surface / forced fallbacks
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_cfg_return_representation_vs_oracle(precision):
+    """``UNet.forward(x, t, labels, return_representation=True)`` (ModelCondition.py:206,225-235):
+    (eps, h) with h the pre-tail activation as NCHW fp32, against the oracle's pre-tail tensor
+    (fp32: max|d| <= 2e-4 on the tiny CFG UNet; bf16: rel-L2 <= 2e-2 on Arch C)."""
+    a = ARCH_TINY_CFG if precision == "fp32" else ARCH_C
+    sd = synthetic_state_dict(a, 0)
+    net = _net(a, precision)
+    gen = torch.Generator().manual_seed(17)
+    x = torch.randn(3, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (3,), generator=gen)
+    lab = torch.tensor([0, 4, 10])
+    eps, rep = net(x.cuda(), t.cuda(), lab.cuda(), return_representation=True)
+    e_only = net(x.cuda(), t.cuda(), lab.cuda())
+    assert torch.equal(eps, e_only)
+    with torch.no_grad():
+        r_eps, r_rep = R.unet_forward(sd, x, t, a.ch, a.ch_mult, a.attn, a.num_res_blocks, labels=lab, cfg=True,
+                                      return_representation=True)
+    assert tuple(rep.shape) == tuple(r_rep.shape) == (3, a.ch * a.ch_mult[0], 32, 32)
+    if precision == "fp32":
+        np.testing.assert_allclose(rep.cpu().numpy(), r_rep.numpy(), atol=EPS_TOL_FP32, rtol=0)
+    else:
+        e = _rel_l2(rep.cpu(), r_rep)
+        print(f"Arch C bf16 pre-tail representation rel-L2 {e:.3e}")
+        assert e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_forced_register_staged_conv_vs_reference(precision):
+    """conv_igemm (the register-staged implicit-GEMM conv that conv_variant = 1 forces for every plain
+    conv: 1x1 shortcuts, q|k|v / proj, 3x3 stride-2 downsamples) on Arch A: fp32 against the
+    reference's own eps (archA_eps.npz, max|d| <= 2e-4), bf16 against the oracle (rel-L2 <= 2e-2).
+    (The other fallback-looking kernels -- head_kernel, tail2_kernel / tail_kernel, attn_kernel -- are
+    the fp32 parity path and run in every fp32 test above.)"""
+    g = golden("archA_eps")
+    x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["t"])
+    rt.set_option("conv_variant", 1)
+    try:
+        net = _net(ARCH_A, precision)
+        eps = net(x.cuda(), t.cuda()).cpu()
+    finally:
+        rt.set_option("conv_variant", 2)
+    if precision == "fp32":
+        np.testing.assert_allclose(eps.numpy(), g["eps"], atol=EPS_TOL_FP32, rtol=0)
+    else:
+        assert _rel_l2(eps, torch.from_numpy(g["eps"])) < REL_L2_BF16

@@ -75,7 +75,7 @@ def test_conv_tile_options():
     """The conv tile switches (itsd_set_option) accept 0 off / 1 auto / 2 whenever eligible and
     reject other values; the switches of kernels that only diagnostic builds contain (the
     superseded 256-pixel generations, conv_pipe_wide, the compile-time ablations) fail loudly in
-    the shipped library. Host-side only (no device call)."""
+    the shipped library; the removed generations are refused. Host-side only (no device call)."""
     if not os.path.exists(rt.LIB_PATH):
         import __graft_entry__
 
@@ -88,9 +88,14 @@ def test_conv_tile_options():
         rt.set_option(key, default)
     rt.set_option("conv_wide", 0)
     rt.set_option("gn_reg", 4)
-    for key, val in (("conv_wide", 1), ("gn_reg", 0), ("gn_reg", 3), ("conv_dbg", 4096 | (2 << 13))):
-        with pytest.raises(rt.ItsdError, match="diagnostic builds only"):
+    for key, val in (("conv_wide", 1), ("gn_reg", 0), ("gn_reg", 3)):  # removed generations (round 4)
+        with pytest.raises(rt.ItsdError, match="removed|only 4"):
             rt.set_option(key, val)
+    rt.set_option("conv_dbg", 1)
+    with pytest.raises(rt.ItsdError, match="diagnostic builds only"):
+        rt.set_option("conv_dbg", 4096 | (2 << 13))
+    # a refused value leaves the previous setting in place (validated before it is stored)
+    assert rt.lib().itsd_set_option(b"conv_dbg", 1) == 0
     rt.set_option("conv_dbg", 0)
 
 

@@ -1,16 +1,17 @@
 #!/bin/bash
-# Resubmit a gpurun call ONLY while the pool reports an infrastructure event before the command ran
-# (box not prepared / taken away / back-off: nothing executed, nothing charged). Any run that
-# executed -- pass or fail -- is returned as is. Usage: tools/gpurun_retry.sh <log> <timeout_s> '<cmd>'
+# Resubmit a gpurun call ONLY while the pool reports that nothing executed (box not prepared / taken
+# away / no box or slot free / back-off: nothing ran, nothing charged). Any run that executed -- pass
+# or fail, whatever its exit code -- is returned as is, so a GPU failure is read, not re-run.
+# Usage: tools/gpurun_retry.sh <log> <timeout_s> '<cmd>'
 log=$1; to=$2; cmd=$3
 for i in 1 2 3 4 5 6; do
   timeout $((to + 900)) /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
-  if grep -q "status=transient\|backing off\|stopped responding while being prepared\|taken away by the GPU service" "$log" && \
-     ! grep -q "status=ok" "$log"; then
-    sleep 60; continue
+  if grep -q "status=transient\|backing off\|stopped responding while being prepared\|taken away by the GPU service\|no box\|no slot" "$log" && \
+     ! grep -q "status=ok\|status=fail" "$log"; then
+    sleep 90; continue
   fi
-  [ $rc -eq 3 ] && { sleep 90; continue; }
   break
 done
 tail -3 "$log"
+exit $rc
