@@ -192,6 +192,7 @@ struct itsd_unet {
   void* zero_page = nullptr;  // 256 KiB of zeros (conv DMA source for padding, conv.hip zero_of_block)
   float* splitk_ws = nullptr;  // split-K partial tiles (shared by all convs: they run in stream order)
   int* tickets = nullptr;      // in-launch split-K counters (conv3x3_gn_p5_kernel), zero between launches
+  int* attn_sync = nullptr;    // attn_block_split_kernel's per-image hand-off counters [nb_max][2] (monotonic)
   static constexpr long long kSplitkCap = 16ll << 20;  // floats (64 MB)
 
   hipStream_t stream = nullptr;
@@ -308,7 +309,7 @@ struct Builder {
   // (2i+py, 2j+px) sees input rows i+dy+py-1 (dy in {0,1}) with the 3x3 taps folded
   // onto them: W'[ph][co][dy][dx][ci] = sum over ky in R(py,dy), kx in R(px,dx) of
   // W[co][ci][ky][kx], R(0,0)={0}, R(0,1)={1,2}, R(1,0)={0,1}, R(1,1)={2}. Sums in fp64.
-  size_t pack_subpix(const float* W, int Cout, int Cin) {
+  size_t pack_subpix(const float* W, int Cout, int Cin, size_t* wfrag = nullptr) {
     static const int lo[2][2] = {{0, 1}, {0, 2}}, hi[2][2] = {{0, 2}, {1, 2}};  // [p][d] -> k range
     const int K = 4 * Cin;
     std::vector<float> tmp((size_t)4 * Cout * K, 0.f);
@@ -324,6 +325,20 @@ struct Builder {
                   acc += W ? (double)W[(((size_t)co * Cin + ci) * 3 + ky) * 3 + kx] : 0.0;
               tmp[((size_t)ph * Cout + co) * K + (dy * 2 + dx) * Cin + ci] = (float)acc;
             }
+    }
+    if (wfrag && u->bf16 && Cout % 32 == 0 && K % 16 == 0) {
+      // the same folded weights in MFMA A-fragment order per phase, [4][Cout/32][K/16][64][8]
+      // (conv3x3_gn_p4_kernel's sub-pixel form): lane L of k-step st holds W'[ph][32 cb + L % 32][16 st + 8 (L / 32) + e]
+      const int nks = K / 16;
+      std::vector<uint16_t> f(tmp.size());
+      for (int ph = 0; ph < 4; ++ph)
+        for (int cb = 0; cb < Cout / 32; ++cb)
+          for (int st = 0; st < nks; ++st)
+            for (int L = 0; L < 64; ++L)
+              for (int e = 0; e < 8; ++e)
+                f[((((size_t)ph * (Cout / 32) + cb) * nks + st) * 64 + L) * 8 + e] =
+                    host_f2bf(tmp[((size_t)ph * Cout + 32 * cb + (L & 31)) * K + 16 * st + 8 * (L >> 5) + e]);
+      *wfrag = ar.add(f.data(), f.size() * 2);
     }
     if (u->bf16) {
       std::vector<uint16_t> b(tmp.size());
@@ -366,13 +381,17 @@ struct Builder {
     if (((A.H * A.W) % 128 && 128 % (A.H * A.W)) || Cin % (8 * epc))
       return conv_layer(s1, -1, name, Cout, 3, 1, 1, 1, Hout, Hout);
     const float* W = get(name + ".weight", (int64_t)Cout * Cin * 9);
-    size_t wt = pack_subpix(W, Cout, Cin);
+    size_t wf = SIZE_MAX;
+    // fragment-ordered copy for conv3x3_gn_p4_kernel's sub-pixel form (input grids 8x8 / 16x16 / 32x32)
+    const bool p4sub = Cout % 128 == 0 && Cin % 64 == 0 && Cin >= 128 && A.H == A.W && (A.W == 8 || A.W == 16 || A.W == 32);
+    size_t wt = pack_subpix(W, Cout, Cin, p4sub ? &wf : nullptr);
     size_t b = f32(name + ".bias", Cout);
     int dst = act(Hout, Hout, Cout);
     if (A.H * A.W < 128) u->acts[dst].spi = 4;  // one statistics slot per (image, phase)
     conv(s1, -1, dst, wt, b, Cout, 3, 1, 1, 1);
     Op& o = u->ops.back();
     o.subpix = 1;
+    o.wfrag = wf;
     return dst;
   }
   size_t concat_f32(const std::vector<const float*>& parts, int n) {
@@ -888,6 +907,13 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.out_stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.scale = (float)std::pow((double)o.C, -0.5);
     a.n = c.nb;
+    // attn_block_split_kernel's slabs in the split-K workspace (ops run in stream order; <= 4 MB of
+    // partial scores at n * G <= 256, then the O slab)
+    if ((long long)c.nb * 64 * o.C * 2 / 4 + (4ll << 20) / 4 <= itsd_unet::kSplitkCap) {
+      a.spart = u->splitk_ws;
+      a.oslab = (bf16_t*)(u->splitk_ws + (4ll << 20) / 4);
+      a.sync = u->attn_sync;
+    }
     e = launch_attn_block(a, o.C, s);
   } else {
     AttnArgs a{};
@@ -1164,6 +1190,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_splitk_inl = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "p4_sub")) {  // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form: 0 off, 1 on
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_sub in [0,1]");
+    itsd::g_p4_sub = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p4_plain")) {  // plain 3x3 stride-1 convs on conv3x3_gn_p4_kernel (halo copies the input)
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_plain in [0,1]");
     itsd::g_p4_plain = value;
@@ -1181,6 +1212,12 @@ int itsd_set_option(const char* key, int value) {
   }
   if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p4 / p5_kernel: 0 off, 1 on
     itsd::g_gn_fold = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_split")) {  // attn_block_split_kernel (an image over G blocks): 0 off, 1 auto, 2 / 4 / 6 forced
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 6)
+      return fail(ITSD_ERR_INVALID, "attn_split in {0, 1, 2, 4, 6}");
+    itsd::g_attn_split = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards
@@ -1247,6 +1284,8 @@ int itsd_unet_create(const itsd_unet_desc* desc, const itsd_tensor_view* weights
   HIPCHK(hipMalloc(&u->splitk_ws, itsd_unet::kSplitkCap * 4));
   HIPCHK(hipMalloc(&u->tickets, itsd::kTicketCap * 4));
   HIPCHK(hipMemset(u->tickets, 0, itsd::kTicketCap * 4));
+  HIPCHK(hipMalloc(&u->attn_sync, (size_t)u->nb_max * 2 * 4));
+  HIPCHK(hipMemset(u->attn_sync, 0, (size_t)u->nb_max * 2 * 4));
   HIPCHK(hipMalloc(&u->proj_buf, (size_t)d.max_batch * u->sumC * 4));
   CHK(alloc_rows(u.get(), std::max(d.max_batch, d.num_labels + 1)));
   if (u->cfg) {
@@ -1267,6 +1306,7 @@ int itsd_unet_destroy(itsd_unet* u) {
   hipFree(u->temb_table); hipFree(u->d_t); hipFree(u->d_nan); hipFree(u->d_run); hipFree(u->x_state); hipFree(u->lab_state); hipFree(u->zero_page);
   hipFree(u->splitk_ws);
   hipFree(u->tickets);
+  hipFree(u->attn_sync);
   if (u->stream) hipStreamDestroy(u->stream);
   if (u->ev_in) hipEventDestroy(u->ev_in);
   if (u->ev_out) hipEventDestroy(u->ev_out);

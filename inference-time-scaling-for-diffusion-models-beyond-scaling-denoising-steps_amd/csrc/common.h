@@ -21,8 +21,10 @@ extern int g_num_cus;       // compute units of the device (persistent grids)
 extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_splitk_inl;     // conv_pipe split-K combined in-launch: 0 off (second launch), 1 on (itsd_set_option "splitk_inl")
 extern int g_p4_plain;      // plain (no GroupNorm) 3x3 stride-1 convs on conv3x3_gn_p4_kernel<W, 2>: 0 off, 1 on (itsd_set_option "p4_plain")
+extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
+extern int g_attn_split;     // attn_block_split_kernel at small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
 // Census (itsd_profile_ops): the first kernel an op launches. Every launch site goes through
@@ -192,6 +194,11 @@ struct AttnBlockArgs {
   float* out_stats;       // [n][2][C] (one slot per image) or null
   float scale;            // C^-0.5
   int n;
+  // attn_block_split_kernel (an image's work over G blocks, small batches): partial-score and O slabs
+  // (write-through hand-offs) and two monotonic counters per image
+  float* spart;           // [n][G][4 tiles][64 lanes][16] fp32
+  bf16_t* oslab;          // [n][64][C] bf16
+  int* sync;              // [n][2], never reset (targets from each block's own add)
 };
 
 struct HeadArgs {

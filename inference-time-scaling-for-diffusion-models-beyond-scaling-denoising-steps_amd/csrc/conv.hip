@@ -51,6 +51,7 @@ int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
+int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
@@ -1229,10 +1230,17 @@ constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 M
 // (W = 32, 16) only. The halo waves are the same.
 constexpr int P16_RING = 2;  // A k32-step slots (divides the 18 k32-steps of a chunk)
 // AB: bit 1 (value 2) = plain conv3x3 (no GroupNorm+SiLU: the halo waves copy the input; shipped, the
-// CFG UpSample's 3x3 conv, conv_p4_plain_selected); the other bits are diagnostic ablations (ITSD_DIAG).
+// CFG UpSample's 3x3 conv, conv_p4_plain_selected); bit 7 (value 128) = the sub-pixel form of a
+// nearest-x2 upsample + conv3x3 (Model.py:121-126; plain): W is the INPUT grid, a tile is (phase, 256
+// input-grid pixels, 128 couts), 4 taps (the phase's 2x2 folded weights, wfrag [4 phases][Cout/32][K/16])
+// at halo offsets (dy + py, dx + px), outputs scattered to (2i + py, 2j + px) and the statistics slots of
+// each (image, phase) (conv_p4_sub_selected); the other bits are diagnostic
+// ablations (ITSD_DIAG).
 template <int W, int AB = 0, bool M16 = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   typedef bf16_t T;
+  constexpr bool SUB = (AB & 128) != 0, PLAIN = SUB || (AB & 2) != 0;
+  constexpr int NTAP = SUB ? 4 : 9, KST = 4 * NTAP;  // taps and 16-deep k-steps of a 64-channel chunk
   constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = GnpCfg<W>::ITEMS, RES = GnpCfg<W>::RES;
   constexpr int W2 = W + 2;
   constexpr int THs = NSEG == 1 ? GNW_BN / W : W;
@@ -1241,8 +1249,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  constexpr int RING = (AB & 64) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
-  static_assert(36 % RING == 0, "ring slots repeat per chunk");
+  constexpr int RING = (AB & 64) ? 4 : (SUB ? 4 : P4_RING), BD = (AB & 32) ? P4_BD + 1 : P4_BD;
+  static_assert(KST % RING == 0, "ring slots repeat per chunk");
+  static_assert(!(SUB && M16), "the sub-pixel form runs the 32x32x16 MFMA path");
   // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]
   __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4 + 4 * 64 * 4];
   char* const rlds = smem + 2 * HALO;
@@ -1257,15 +1266,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.Hout;
   const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
-  const int nTC = a.Cout / CONV_BM, NT = (a.M / GNW_BN) * nTC;
+  const int nTC = a.Cout / CONV_BM, nPT = a.M / GNW_BN, NT = (SUB ? 4 : 1) * nPT * nTC;
   const int G = gridDim.x, b = blockIdx.x;
   // block b walks the contiguous tile range [tb0, tb0 + ntiles) (cout tile fastest): its tiles share
   // pixel tiles and images, so a gn_fold block reduces an image's statistics once for all of them
   const int tb0 = (int)(((long long)b * NT) / G);
   const int ntiles = (int)(((long long)(b + 1) * NT) / G) - tb0;
   const int nstages = ntiles * ncc;
-  auto tile_p = [&](int k) { return ((tb0 + k) / nTC) * GNW_BN; };
+  // tile t = ((phase * nPT) + pixel tile) * nTC + cout tile (SUB: phase slowest, so a block's contiguous
+  // range keeps one phase's weights)
+  auto tile_p = [&](int k) { return (SUB ? ((tb0 + k) / nTC) % nPT : (tb0 + k) / nTC) * GNW_BN; };
   auto tile_c = [&](int k) { return ((tb0 + k) % nTC) * CONV_BM; };
+  auto tile_ph = [&](int k) { return SUB ? (tb0 + k) / (nTC * nPT) : 0; };
+  // SUB: output NHWC row of input-grid pixel p of phase ph: (img, 2i + py, 2j + px) of the 2x grid
+  auto orow = [&](int p, int ph) -> size_t {
+    if constexpr (!SUB) return (size_t)p;
+    const int HWi = H * W, img = p / HWi, rem = p - img * HWi, i = rem / W, j = rem - i * W;
+    return ((size_t)img * 2 * H + 2 * i + (ph >> 1)) * (2 * W) + 2 * j + (ph & 1);
+  };
 #ifdef ITSD_STAMPS
   // MFMA waves: 0 chunk compute, 1 barrier wait, 6 epilogues, 7 total; halo waves: 3 stage
   // transforms (incl. next-stage load issue), 1 barrier wait, 5 prologue (stage 0), 7 total
@@ -1445,9 +1463,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
       hb[j] = seg * HS + oy * W2 + (rem - oy * W);
     }
-    const size_t ablk = (size_t)(9 * kpt) * 1024;  // one 32-cout block of fragments
+    const size_t ablk = (size_t)(NTAP * kpt) * 1024;  // one 32-cout block of fragments
     auto abase_of = [&](int k) {
-      return (const char*)a.wfrag + (size_t)((tile_c(k) >> 5) + 2 * wm) * ablk + lane * 16;
+      return (const char*)a.wfrag + ((size_t)tile_ph(k) * (a.Cout >> 5) + (tile_c(k) >> 5) + 2 * wm) * ablk + lane * 16;
     };
     f32x16 acc[2][4];
 #pragma unroll
@@ -1491,7 +1509,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     if constexpr (RES) init_acc(0);
     int q = 0;     // stage (chunk) counter of this block
     for (int k = 0; k < ntiles; ++k) {
-      const int tileP = tile_p(k), tileC = tile_c(k);
+      const int tileP = tile_p(k), tileC = tile_c(k), tph = tile_ph(k);
       const char* ab = abase_of(k);
       const char* abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
       for (int cc = 0; cc < ncc; ++cc, ++q) {
@@ -1509,7 +1527,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         bf16x8 fb[BD][4];
         auto rd = [&](int st, int buf) __attribute__((always_inline)) {
           if ((st & 3) == 0) {
-            const int tap = st >> 2, ky = tap / 3, kx = tap - ky * 3;
+            const int tap = st >> 2;
+            // SUB: tap (dy, dx) of phase (py, px) reads input offset (dy + py - 1, dx + px - 1)
+            const int ky = SUB ? (tap >> 1) + (tph >> 1) : tap / 3, kx = SUB ? (tap & 1) + (tph & 1) : tap - (tap / 3) * 3;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               int h = hb[j] + ky * W2 + kx;
@@ -1527,11 +1547,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         for (int s0 = 0; s0 < BD - 1; ++s0) rd(s0, s0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int step = 0; step < 36; ++step) {
+        for (int step = 0; step < KST; ++step) {
           const int pf = step + RING - 1;
-          if (pf < 36) load_a(cb, pf, ra[pf % RING]);
-          else load_a(nb, pf - 36, ra[pf % RING]);
-          if (step + BD - 1 < 36) rd(step + BD - 1, (step + BD - 1) % BD);
+          if (pf < KST) load_a(cb, pf, ra[pf % RING]);
+          else load_a(nb, pf - KST, ra[pf % RING]);
+          if (step + BD - 1 < KST) rd(step + BD - 1, (step + BD - 1) % BD);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % RING][i]);
@@ -1648,7 +1668,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
             o[2 + d] = sw[1];
           }
           const int c8 = wmi * 32 + 8 * (gp + hh);
-          *(u32x4*)((T*)a.out + (size_t)(tileP + p) * a.Cout + tileC + c8) = o;
+          *(u32x4*)((T*)a.out + orow(tileP + p, tph) * a.Cout + tileC + c8) = o;
         }
         if (a.stats && ((NSEG == 1 && j == 3) || (NSEG != 1 && (j & 1)))) {
           float v[32];
@@ -1683,7 +1703,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
           halve(std::integral_constant<int, 1>{});
           {
             constexpr int SLOT = NSEG == 1 ? 128 : 64;
-            const long long slot = (long long)(tileP + wn * 128 + (NSEG == 1 ? 0 : (j >> 1) * 64)) / SLOT;
+            long long slot = (long long)(tileP + wn * 128 + (NSEG == 1 ? 0 : (j >> 1) * 64)) / SLOT;
+            // SUB (W = 8: 64-pixel phase images): one statistics slot per (image, phase)
+            if constexpr (SUB) slot = slot * 4 + tph;
             const int e = rl & 15, co = wmi * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
             a.stats[(slot * 2 + (rl >> 4)) * a.Cout + tileC + co] = v[0];
           }
@@ -1802,7 +1824,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
       ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
     }
-    if constexpr ((AB & 2) == 0) cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
+    if constexpr (!PLAIN) cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
     simg = img0 + sg;
   };
   // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
@@ -1869,7 +1891,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // sum (b3 = 0) or sum of squares of couts 8u + 4 b4 + 2 b5 + {0, 1}
   auto drain = [&](int kd) __attribute__((always_inline)) {
     if constexpr (RES) {
-      const int tileP = tile_p(kd), tileC = tile_c(kd), u = lane & 7;
+      const int tileP = tile_p(kd), tileC = tile_c(kd), u = lane & 7, dph = tile_ph(kd);
       float v[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = 0.f;
@@ -1877,7 +1899,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       for (int i = 0; i < 16; ++i) {
         const int row = 128 * ds + 8 * i + (lane >> 3);
         const u32x4 d = *(const u32x4*)(rlds + dh * 32768 + row * 128 + ((u ^ ((row >> 1) & 7)) << 4));
-        *(u32x4*)((T*)a.out + (size_t)(tileP + row) * a.Cout + tileC + dh * 64 + u * 8) = d;
+        *(u32x4*)((T*)a.out + orow(tileP + row, dph) * a.Cout + tileC + dh * 64 + u * 8) = d;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
           const float lo = __uint_as_float(d[w] << 16), hi = __uint_as_float(d[w] & 0xffff0000u);
@@ -1910,7 +1932,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         halve(std::integral_constant<int, 8>{}, 8);
         halve(std::integral_constant<int, 16>{}, 4);
         halve(std::integral_constant<int, 32>{}, 2);
-        const long long slot = (long long)tileP / 128 + ds;
+        long long slot = (long long)tileP / 128 + ds;
+        if constexpr (SUB) {  // (image, phase, 128-pixel slot of the phase image): the 2x grid has 4x the slots
+          const int HWi = H * W, spp = HWi / 128, img = tileP / HWi;
+          slot = (long long)img * 4 * spp + dph * spp + (tileP - img * HWi) / 128 + ds;
+        }
         const int co = dh * 64 + 8 * u + 4 * ((lane >> 4) & 1) + 2 * (lane >> 5);
         *(float2*)(a.stats + (slot * 2 + ((lane >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
       }
@@ -1923,7 +1949,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // the loaded stage's coefficients c from cn: gn_coef rows (a0..a7, b0..b7), or (gn_fold) gamma0..7,
   // beta0..7 with the group statistics in gsw: a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula)
   auto prescale = [&]() __attribute__((always_inline)) {  // scalar multiplies (packed f32 is costly here)
-    if constexpr ((AB & 2) != 0) return;  // plain conv: no GroupNorm coefficients
+    if constexpr (PLAIN) return;  // plain conv: no GroupNorm coefficients
     if (a.gn_fold) {
       // group of channel c = floor((c + 0.5) / gsz) by a reciprocal (exact: c < 2^11, gsz <= 64)
       const int c0 = ccL * 64 + 8 * lch;
@@ -1944,7 +1970,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     }
   };
   auto load_cn = [&](int ccx) __attribute__((always_inline)) {  // (stage coefficients or affine, as above)
-    if constexpr ((AB & 2) != 0) return;
+    if constexpr (PLAIN) return;
     if (a.gn_fold) {
       const int c0 = ccx * 64 + 8 * lch;
       cn[0] = *(const f32x4*)(a.gn_gamma + c0);
@@ -1980,7 +2006,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     for (int j = 0; j < ITEMS; ++j) {
       const uint32_t zm = (uint32_t)__builtin_amdgcn_sbfe(inm, j, 1);  // 0 (padding) or ~0
       uint32_t yw[4];
-      if constexpr ((AB & 2) != 0) {
+      if constexpr (PLAIN) {
 #pragma unroll
         for (int w = 0; w < 4; ++w) yw[w] = h[j][w] & zm;
       } else
@@ -2913,6 +2939,16 @@ bool conv_p4_plain_selected(const ConvArgs& a) {
          (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
 }
 
+// A nearest-x2 upsample conv (sub-pixel phases, subpix 1) on conv3x3_gn_p4_kernel<W, 128>? W = the input
+// grid (8 / 16 / 32); auto where the 4 phases x 256-pixel tiles x 128-cout tiles fill the chip (>= 192)
+bool conv_p4_sub_selected(const ConvArgs& a) {
+  if (!g_p4_sub || a.subpix != 1 || !a.wfrag || a.ksize != 2 || a.resid || a.vt_out || !a.zero || a.gn_coef ||
+      a.Hout != a.Wout || !(a.Wout == 8 || a.Wout == 16 || a.Wout == 32) || a.Cout % CONV_BM || a.C1 % 64 ||
+      a.C2 % 64 || a.C1 + a.C2 < 128 || a.K != 4 * (a.C1 + a.C2) || a.M % GNW_BN)
+    return false;
+  return 4LL * (a.M / GNW_BN) * (a.Cout / CONV_BM) >= 192;
+}
+
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p5_kernel?
 bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
@@ -3029,6 +3065,15 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.subpix) {
     if (!pipe || !lin || a.ksize != (a.subpix == 2 ? 3 : 2) || ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
       return hipErrorInvalidValue;
+    if constexpr (sizeof(T) == 2) {
+      if (conv_p4_sub_selected(a)) {  // 4 phases x pixel tiles x cout tiles, persistent
+        const dim3 gp(std::min(4 * (a.M / GNW_BN) * (a.Cout / CONV_BM), g_num_cus));
+        if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 128>), gp, dim3(512), 0, s, a);
+        else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 128>), gp, dim3(512), 0, s, a);
+        else ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 128>), gp, dim3(512), 0, s, a);
+        return hipGetLastError();
+      }
+    }
     grid.z = 4;
     ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();

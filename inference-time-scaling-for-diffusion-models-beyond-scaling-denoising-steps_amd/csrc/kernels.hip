@@ -4,6 +4,7 @@
 // verifiers, and the counter-based Philox normal generator.
 #include <math.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -704,6 +705,344 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   ATL(7);
 }
 
+// ---------------------------------------------------------------------------- fused AttnBlock over G blocks
+// attn_block_split_kernel<C, G>: attn_block_kernel's image spread over G blocks for small batches (the
+// 8-GPU shard runs N = 32: one block per image left 224 of 256 CUs idle while every block streamed all
+// 1.2 MB of the block's weights). Block (img, g) owns channel blocks [g CBg, (g+1) CBg),
+// CBg = C / 32 / G, and streams only those weight rows:
+//   0. GroupNorm + hn as attn_block_kernel (every block: hn is the K operand of every projection);
+//   1. its V^T, Q, K channel slices (hn W^T + b) -> LDS;
+//   2. its partial scores S_g^T = K_g Q_g^T (keys x queries, fp32) -> write-through slab, counter;
+//      every block waits for the image's G partials, sums them in g order 0..G-1 (the same bits in every
+//      block, whichever arrives last) -> softmax -> P (bf16), as attn_block_kernel;
+//   3. O^T of its channels = V_g^T P^T -> write-through slab [img][token][C], counter; waits for all G;
+//   4. out = x + O Wp^T + bp for its output channels (full O from the slab), its channels' GroupNorm
+//      statistics (per channel: no cross-block sum).
+// Roundings as attn_block_kernel (hn, q / k / v, P, O in bf16); only S is summed in another order (G
+// partial sums), so it agrees with attn_block_kernel within bf16 tolerance, not bit for bit.
+// Hand-offs: MI355X_MICROARCH.md visibility table, row 1 (sc1 stores; every storing wave waits
+// vmcnt(0); a workgroup barrier; one agent-scope atomic add per block; one lane polls with sc1 loads
+// (s_sleep, bounded); a workgroup barrier; every load of the handed-off bytes an sc1 load). The counters
+// only grow: a block's target is (old / G + 1) * G from the value its own add returned (launches on a
+// stream never overlap). Waiting blocks need the whole grid resident: the host launches it only when
+// n * G <= CUs (one 512-thread block per CU).
+template <int C, int G>
+__global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs a) {
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBg = CB / G, CW = CBg * 32, PF = 8;
+  static_assert(CB % G == 0 && C % 128 == 0, "G divides the channel blocks");
+  constexpr int QROW = CW * 2 + 16;  // Q_g / K_g row (bytes): padded so 16-B reads of 16 rows are conflict-free
+  constexpr int R_VT = S * C * 2, R_Q = R_VT + CW * 128, R_K = R_Q + S * QROW, R_SM = R_K + S * QROW;
+  constexpr int R_PM = R_SM + S * (S + 4) * 4, R_GS = R_PM + S * 128, R_ST = R_GS + 32 * 2 * 4;
+  __shared__ __attribute__((aligned(16))) char sm[R_ST + 2 * 2 * CW * 4];
+  const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int img = blockIdx.x / G, g = blockIdx.x - (blockIdx.x / G) * G;
+  const bf16_t* x = a.x + (size_t)img * S * C;
+  auto rowc = [](int r, int ch, int rowbytes) { return r * rowbytes + ((ch ^ (r & 15)) << 4); };
+  auto row64 = [](int r, int ch) { return r * 128 + ((ch ^ ((r >> 1) & 7)) << 4); };
+  auto frag = [&](const bf16_t* W, int cb, int st) -> const bf16x8* {
+    return (const bf16x8*)((const char*)W + ((size_t)cb * KS + st) * 1024 + lane * 16);
+  };
+  // ---- 0. GroupNorm statistics and hn (attn_block_kernel's phase 0)
+  constexpr int XU = S * (C / 8) / 512;
+  u32x4 xv[XU];
+#pragma unroll
+  for (int i = 0; i < XU; ++i) {
+    const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8);
+    xv[i] = *(const u32x4*)(x + (size_t)t * C + ch * 8);
+  }
+  float* gs = (float*)(sm + R_GS);
+  if (tid < 256) {
+    const int gr = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
+    double s = 0.0, q = 0.0;
+    for (int k = l8; k < n_it; k += 8) {
+      const int c = gr * gsz + k / a.spi;
+      const long long sl = (long long)img * a.spi + k % a.spi;
+      s += (double)a.st[(sl * 2) * C + c];
+      q += (double)a.st[(sl * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      q += __shfl_xor(q, o, 64);
+    }
+    if (l8 == 0) {
+      const double E = (double)gsz * S, mean = s / E;
+      double var = q / E - mean * mean;
+      var = var > 0.0 ? var : 0.0;
+      gs[2 * gr] = (float)mean;
+      gs[2 * gr + 1] = (float)(1.0 / sqrt(var + 1e-5));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < XU; ++i) {
+    const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8), c0 = ch * 8;
+    uint32_t o[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      float y[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = c0 + 2 * e2 + h2, gg = c / (C / 32);
+        const float mean = gs[2 * gg], rstd = gs[2 * gg + 1];
+        const float sc = rstd * a.gamma[c];
+        const float xf = __uint_as_float(h2 ? (xv[i][e2] & 0xffff0000u) : (xv[i][e2] << 16));
+        y[h2] = xf * sc + (a.beta[c] - mean * sc);
+      }
+      o[e2] = pk_bf16(y[0], y[1]);
+    }
+    *(u32x4*)(sm + rowc(t, ch, C * 2)) = u32x4{o[0], o[1], o[2], o[3]};
+  }
+  __syncthreads();
+  auto hn_frag = [&](int r, int st) { return *(const bf16x8*)(sm + rowc(r, 2 * st + hh, C * 2)); };
+  // weight-stream unit: one 32-channel block of a projection over both token blocks (fragments loaded once)
+  auto unit = [&](const bf16_t* W, int frow, f32x16 (&acc)[2], auto vform) __attribute__((always_inline)) {
+    constexpr bool VF = decltype(vform)::value;  // true: D[token][c] (A = hn); false: D[c][token] (A = W)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tb][r] = 0.f;
+    bf16x8 fw[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) fw[p] = *frag(W, frow, p);
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const bf16x8 cur = fw[st % PF];
+      if (st + PF < KS) fw[st % PF] = *frag(W, frow, st + PF);
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb) {
+        const bf16x8 h0 = hn_frag(32 * tb + rl, st);
+        if constexpr (VF) acc[tb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h0, cur, acc[tb], 0, 0, 0);
+        else acc[tb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, h0, acc[tb], 0, 0, 0);
+      }
+    }
+  };
+  // ---- 1. this block's V^T, Q, K slices: units u = kind * CBg + cbl (kind 0 V, 1 Q, 2 K)
+  for (int u = w; u < 3 * CBg; u += 8) {
+    const int kind = u / CBg, cbl = u - kind * CBg, cb = g * CBg + cbl;
+    f32x16 acc[2];
+    if (kind == 0) {
+      unit(a.wqkv, 2 * CB + cb, acc, std::true_type{});
+      // lane: channel 32 cb + rl, tokens 32 tb + 8 q + 4 hh + e -> V^T row (local channel), 4 tokens a store
+      const float bv = a.bqkv[2 * C + 32 * cb + rl];
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *(uint2*)(sm + R_VT + row64(32 * cbl + rl, 4 * tb + q) + 8 * hh) =
+              uint2{pk_bf16(acc[tb][4 * q] + bv, acc[tb][4 * q + 1] + bv), pk_bf16(acc[tb][4 * q + 2] + bv, acc[tb][4 * q + 3] + bv)};
+    } else {
+      unit(a.wqkv, (kind - 1) * CB + cb, acc, std::false_type{});
+      // lane: token 32 tb + rl, channels 32 cb + 8 q + 4 hh + e -> Q_g / K_g [token][local channel]
+      char* dst = sm + (kind == 1 ? R_Q : R_K);
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cl = 32 * cbl + 8 * q + 4 * hh;
+          const f32x4 bq = *(const f32x4*)(a.bqkv + (kind - 1) * C + g * CW + cl);
+          *(uint2*)(dst + (32 * tb + rl) * QROW + cl * 2) =
+              uint2{pk_bf16(acc[tb][4 * q] + bq[0], acc[tb][4 * q + 1] + bq[1]), pk_bf16(acc[tb][4 * q + 2] + bq[2], acc[tb][4 * q + 3] + bq[3])};
+        }
+    }
+  }
+  __syncthreads();
+  // ---- 2. partial scores S_g^T[key][query] over this block's channels (waves 0..3: tile w), write-through
+  const uint32_t sp_bytes = (uint32_t)std::min<long long>((long long)a.n * G * 4 * 1024 * 4, 0x7fffffffLL);
+  const __amdgpu_buffer_rsrc_t sp = __builtin_amdgcn_make_buffer_rsrc(a.spart, (short)0, (int)sp_bytes, 0x00020000);
+  if (w < 4) {
+    const int key = 32 * (w >> 1) + rl, qry = 32 * (w & 1) + rl;
+    f32x16 sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < CW / 16; ++st) {
+      const bf16x8 kf = *(const bf16x8*)(sm + R_K + key * QROW + (2 * st + hh) * 16);
+      const bf16x8 qf = *(const bf16x8*)(sm + R_Q + qry * QROW + (2 * st + hh) * 16);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf, sacc, 0, 0, 0);
+    }
+    const uint32_t off = (uint32_t)((((size_t)img * G + g) * 4 + w) * 1024 + lane * 16) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(sacc[4 * q]), __float_as_uint(sacc[4 * q + 1]),
+                                                   __float_as_uint(sacc[4 * q + 2]), __float_as_uint(sacc[4 * q + 3])},
+                                             sp, off + q * 16, 0, 16);
+  }
+  // hand-off: this block's stores drained, one add, one lane polls until the image's G blocks have added
+  auto handoff = [&](int* cnt) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int target = (old / G + 1) * G;
+      for (int it = 0; it < (1 << 22); ++it) {  // bounded: a grid that is not co-resident cannot hang the GPU
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+  };
+  handoff(a.sync + 2 * img);
+  // every block: S = sum of the G partials in g order (waves 0..3, their tile), scaled -> Sm [query][key]
+  float* const Sm = (float*)(sm + R_SM);
+  char* const Pm = sm + R_PM;
+  if (w < 4) {
+    f32x16 sacc;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const uint32_t off = (uint32_t)((((size_t)img * G + gg) * 4 + w) * 1024 + lane * 16) * 4;
+      u32x4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = __builtin_amdgcn_raw_buffer_load_b128(sp, off + q * 16, 0, 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          sacc[4 * q + e] = gg == 0 ? __uint_as_float(v[q][e]) : sacc[4 * q + e] + __uint_as_float(v[q][e]);
+    }
+    const int qry = 32 * (w & 1) + rl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Sm[qry * (S + 4) + 32 * (w >> 1) + 8 * q + 4 * hh + e] = sacc[4 * q + e] * a.scale;
+  }
+  __syncthreads();
+  {  // ---- softmax over keys (attn_block_kernel's phase 3): 8 lanes a query, 8 keys a lane
+    const int qry = tid >> 3, k0 = (tid & 7) * 8;
+    float v[8], m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = Sm[qry * (S + 4) + k0 + e];
+      m = fmaxf(m, v[e]);
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = expf(v[e] - m);
+      sum += v[e];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    const float inv = 1.0f / sum;
+    *(u32x4*)(Pm + row64(qry, tid & 7)) =
+        u32x4{pk_bf16(v[0] * inv, v[1] * inv), pk_bf16(v[2] * inv, v[3] * inv), pk_bf16(v[4] * inv, v[5] * inv),
+              pk_bf16(v[6] * inv, v[7] * inv)};
+  }
+  __syncthreads();
+  // ---- 3. O^T of this block's channels = V_g^T P^T: tiles (local channel block, query block) -> O slab
+  const uint32_t o_bytes = (uint32_t)std::min<long long>((long long)a.n * S * C * 2, 0x7fffffffLL);
+  const __amdgpu_buffer_rsrc_t osl = __builtin_amdgcn_make_buffer_rsrc(a.oslab, (short)0, (int)o_bytes, 0x00020000);
+  for (int tile = w; tile < 2 * CBg; tile += 8) {
+    const int cbl = tile >> 1, q = 32 * (tile & 1) + rl;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const bf16x8 p0 = *(const bf16x8*)(Pm + row64(q, 2 * st + hh));
+      const bf16x8 vf = *(const bf16x8*)(sm + R_VT + row64(32 * cbl + rl, 2 * st + hh));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, p0, acc, 0, 0, 0);
+    }
+    // lane: query q, channels g CW + 32 cbl + 8 r4 + 4 hh + e (4 consecutive: one 8-B store)
+    typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const int c = g * CW + 32 * cbl + 8 * r4 + 4 * hh;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{pk_bf16(acc[4 * r4], acc[4 * r4 + 1]), pk_bf16(acc[4 * r4 + 2], acc[4 * r4 + 3])},
+                                            osl, (uint32_t)((((size_t)img * S + q) * C + c) * 2), 0, 16);
+    }
+  }
+  handoff(a.sync + 2 * img + 1);
+  // the full O [token][C] (every block's slice) -> hn's rows (hn is dead since phase 1)
+  for (int i = tid; i < S * (C / 8); i += 512) {
+    const int t = i / (C / 8), ch = i - t * (C / 8);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(osl, (uint32_t)((((size_t)img * S + t) * C + ch * 8) * 2), 0, 16);
+    *(u32x4*)(sm + rowc(t, ch, C * 2)) = v;
+  }
+  __syncthreads();
+  // ---- 4. out = x + O Wp^T + bp for this block's output channels; statistics of its channels
+  float* const spart = (float*)(sm + R_ST);  // [token block][2][CW]
+  bf16_t* out = a.out + (size_t)img * S * C;
+  for (int cbl = w; cbl < CBg; cbl += 8) {
+    const int cb = g * CBg + cbl;
+    f32x16 acc[2];
+    unit(a.wp, cb, acc, std::false_type{});  // D[c'][token]
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const int tk = 32 * tb + rl;
+      float v[32];
+      uint32_t wv[4][2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 32 * cb + 8 * q + 4 * hh;
+        const f32x4 bb = *(const f32x4*)(a.bp + c);
+        const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
+        const float v0 = acc[tb][4 * q + 0] + bb[0] + __uint_as_float(rr.x << 16);
+        const float v1 = acc[tb][4 * q + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
+        const float v2 = acc[tb][4 * q + 2] + bb[2] + __uint_as_float(rr.y << 16);
+        const float v3 = acc[tb][4 * q + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
+        wv[q][0] = pk_bf16(v0, v1);
+        wv[q][1] = pk_bf16(v2, v3);
+        const float r0 = __uint_as_float(wv[q][0] << 16), r1 = __uint_as_float(wv[q][0] & 0xffff0000u);
+        const float r2 = __uint_as_float(wv[q][1] << 16), r3 = __uint_as_float(wv[q][1] & 0xffff0000u);
+        v[4 * q + 0] = r0; v[16 + 4 * q + 0] = r0 * r0;
+        v[4 * q + 1] = r1; v[16 + 4 * q + 1] = r1 * r1;
+        v[4 * q + 2] = r2; v[16 + 4 * q + 2] = r2 * r2;
+        v[4 * q + 3] = r3; v[16 + 4 * q + 3] = r3 * r3;
+      }
+#pragma unroll
+      for (int gp = 0; gp < 4; gp += 2) {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto swp = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+          o[d] = swp[0];
+          o[2 + d] = swp[1];
+        }
+        *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
+      }
+      if (a.out_stats) {
+        auto xchg = [](float xf, auto wc) {
+          constexpr int wd = decltype(wc)::value;
+          const int xi = __builtin_bit_cast(int, xf);
+          int r;
+          if constexpr (wd == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+          else if constexpr (wd == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+          else if constexpr (wd == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+          else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (wd << 10));
+          return __builtin_bit_cast(float, r);
+        };
+        auto halve = [&](auto wc) {
+          constexpr int wd = decltype(wc)::value;
+          const bool up = (rl & wd) != 0;
+#pragma unroll
+          for (int ii = 0; ii < wd; ++ii) {
+            const float lo = v[ii], hi = v[ii + wd];
+            v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+          }
+        };
+        halve(std::integral_constant<int, 16>{});
+        halve(std::integral_constant<int, 8>{});
+        halve(std::integral_constant<int, 4>{});
+        halve(std::integral_constant<int, 2>{});
+        halve(std::integral_constant<int, 1>{});
+        const int e = rl & 15, col = 32 * cbl + 8 * (e >> 2) + 4 * hh + (e & 3);
+        spart[(tb * 2 + (rl >> 4)) * CW + col] = v[0];
+      }
+    }
+  }
+  if (a.out_stats) {
+    __syncthreads();
+    for (int i = tid; i < 2 * CW; i += 512) {  // (sum | sum of squares) x local channel: token block 0 + block 1
+      const int half = i / CW, cl = i - half * CW;
+      a.out_stats[(long long)img * 2 * C + half * C + g * CW + cl] = spart[i] + spart[2 * CW + i];
+    }
+  }
+}
+
 #ifdef ITSD_STAMPS
 extern "C" int itsd_debug_stamps_attn(unsigned long long* host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
@@ -711,7 +1050,25 @@ extern "C" int itsd_debug_stamps_attn(unsigned long long* host) {
 }
 #endif
 
+int g_attn_split = 1;  // attn_block_split_kernel for small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
+// G blocks per image for attn_block_split_kernel at batch n (0: one block per image, attn_block_kernel):
+// the largest of 6 / 4 / 2 that keeps the grid co-resident (n * G <= CUs, one block per CU)
+int attn_split_g(int n, int C) {
+  if (C != 384 || !g_attn_split) return 0;
+  const int opts[3] = {6, 4, 2};
+  for (int G : opts)
+    if ((g_attn_split == 1 || g_attn_split == G) && (long long)n * G <= g_num_cus) return G;
+  return 0;
+}
+
 hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
+  if (a.spart && a.oslab && a.sync) {
+    const int G = attn_split_g(a.n, C);
+    if (G == 6) ITSD_LAUNCH((attn_block_split_kernel<384, 6>), dim3(a.n * 6), dim3(512), 0, s, a);
+    else if (G == 4) ITSD_LAUNCH((attn_block_split_kernel<384, 4>), dim3(a.n * 4), dim3(512), 0, s, a);
+    else if (G == 2) ITSD_LAUNCH((attn_block_split_kernel<384, 2>), dim3(a.n * 2), dim3(512), 0, s, a);
+    if (G) return hipGetLastError();
+  }
   if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(512), 0, s, a);
   else if (C == 256) ITSD_LAUNCH(attn_block_kernel<256>, dim3(a.n), dim3(512), 0, s, a);
   else if (C == 128) ITSD_LAUNCH(attn_block_kernel<128>, dim3(a.n), dim3(512), 0, s, a);

@@ -302,7 +302,7 @@ def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt):
         assert (out - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
 
 
-_TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 4}
+_TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 4, "p4_sub": 1}
 
 
 def _eps_with(net, x, t, **opts):
@@ -407,6 +407,35 @@ def test_subpixel_upsample_convs_at_every_level(precision):
         assert (eps - ref).abs().max().item() < 2e-4
     else:
         assert _rel_l2(eps, ref) < REL_L2_BF16
+
+
+@pytest.mark.parametrize("n", [64, 256])
+def test_p4_subpixel_upsample_convs_vs_conv_pipe_and_oracle(n):
+    """The 16x16 -> 32x32 and 8x8 -> 16x16 nearest-x2 upsample convs (Model.py:121-126) on
+    conv3x3_gn_p4_kernel's sub-pixel form (AB = 128: 4 phases x 256 input-grid pixels x 128 couts per
+    tile, the phase's 2x2 folded taps, outputs scattered to (2i + py, 2j + px), one GroupNorm statistics
+    slot per (image, phase, 128 pixels)) against the same GEMMs on conv_pipe (p4_sub = 0; the k order
+    differs: chunk-major vs tap-major): deterministic, within 1e-2 relative L2 of each other and within
+    the bf16 bound of the oracle. (The 4x4 -> 8x8 upsample stays on conv_pipe: p4 has no 4x4 form.)"""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(500 + n)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, 1000, (n,), generator=gen)
+    x, t = xc.cuda(), tc.cuda()
+    ops = net.native(n).profile_ops(x, t.to(torch.int32))
+    ups = {o["H"]: o["kernel"] for o in ops if o["kind"] == "conv" and o["stride_up"] == 11}
+    assert "conv3x3_gn_p4_kernel<16, 128>" in ups[32] and "conv3x3_gn_p4_kernel<8, 128>" in ups[16], ups
+    assert "conv_pipe" in ups[8], ups
+    sub = _eps_with(net, x, t)
+    assert torch.equal(sub, _eps_with(net, x, t))
+    pipe = _eps_with(net, x, t, p4_sub=0)
+    idx = [0, n // 2, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx])
+    d, e = _rel_l2(sub, pipe), _rel_l2(sub[idx], ref)
+    print(f"n={n}: p4 sub-pixel vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e} (conv_pipe {_rel_l2(pipe[idx], ref):.2e})")
+    assert d < 1e-2 and e < REL_L2_BF16
 
 
 def test_forward_bf16_full_batch_vs_oracle_subset():
