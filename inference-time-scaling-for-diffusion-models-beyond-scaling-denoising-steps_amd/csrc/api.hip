@@ -31,6 +31,8 @@ bool attn_flash_ok(int S, int C);
 bool attn_block_ok(int S, int C);
 hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
 int g_attn_fuse = 1;  // fused AttnBlock kernel where it applies (itsd_set_option "attn_fuse", read at create)
+int g_tap_prune = 1;   // drop conv taps that read only padding for every output pixel ("tap_prune", read at create)
+int g_down_merge = 1;  // CFG DownSample c1 (3x3) + c2 (5x5) as one 5x5 conv ("down_merge", read at create)
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
 hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
@@ -305,6 +307,22 @@ struct Builder {
             }
     return ar.add(b.data(), b.size() * 2);
   }
+  // Phase weights [4][Cout][K] (fp32) in MFMA A-fragment order per phase, [4][Cout/32][K/16][64][8]
+  // (conv3x3_gn_p4_kernel's sub-pixel form): lane L of k-step st holds W'[ph][32 cb + L % 32][16 st + 8 (L / 32) + e].
+  // SIZE_MAX unless bf16 with Cout % 32 == 0 and K % 16 == 0.
+  size_t frag4(const std::vector<float>& tmp, int Cout, int K) {
+    if (!u->bf16 || Cout % 32 || K % 16) return SIZE_MAX;
+    const int nks = K / 16;
+    std::vector<uint16_t> f(tmp.size());
+    for (int ph = 0; ph < 4; ++ph)
+      for (int cb = 0; cb < Cout / 32; ++cb)
+        for (int st = 0; st < nks; ++st)
+          for (int L = 0; L < 64; ++L)
+            for (int e = 0; e < 8; ++e)
+              f[((((size_t)ph * (Cout / 32) + cb) * nks + st) * 64 + L) * 8 + e] =
+                  host_f2bf(tmp[((size_t)ph * Cout + 32 * cb + (L & 31)) * K + 16 * st + 8 * (L >> 5) + e]);
+    return ar.add(f.data(), f.size() * 2);
+  }
   // Nearest-x2 upsample + 3x3 conv (Model.py:123-125) as 4 sub-pixel phases: output
   // (2i+py, 2j+px) sees input rows i+dy+py-1 (dy in {0,1}) with the 3x3 taps folded
   // onto them: W'[ph][co][dy][dx][ci] = sum over ky in R(py,dy), kx in R(px,dx) of
@@ -326,20 +344,7 @@ struct Builder {
               tmp[((size_t)ph * Cout + co) * K + (dy * 2 + dx) * Cin + ci] = (float)acc;
             }
     }
-    if (wfrag && u->bf16 && Cout % 32 == 0 && K % 16 == 0) {
-      // the same folded weights in MFMA A-fragment order per phase, [4][Cout/32][K/16][64][8]
-      // (conv3x3_gn_p4_kernel's sub-pixel form): lane L of k-step st holds W'[ph][32 cb + L % 32][16 st + 8 (L / 32) + e]
-      const int nks = K / 16;
-      std::vector<uint16_t> f(tmp.size());
-      for (int ph = 0; ph < 4; ++ph)
-        for (int cb = 0; cb < Cout / 32; ++cb)
-          for (int st = 0; st < nks; ++st)
-            for (int L = 0; L < 64; ++L)
-              for (int e = 0; e < 8; ++e)
-                f[((((size_t)ph * (Cout / 32) + cb) * nks + st) * 64 + L) * 8 + e] =
-                    host_f2bf(tmp[((size_t)ph * Cout + 32 * cb + (L & 31)) * K + 16 * st + 8 * (L >> 5) + e]);
-      *wfrag = ar.add(f.data(), f.size() * 2);
-    }
+    if (wfrag) *wfrag = frag4(tmp, Cout, K);
     if (u->bf16) {
       std::vector<uint16_t> b(tmp.size());
       for (size_t i = 0; i < tmp.size(); ++i) b[i] = host_f2bf(tmp[i]);
@@ -351,22 +356,25 @@ struct Builder {
   // sub-pixel phases: output (2m+ry, 2n+rx) = sum over input (m+dy, n+dx), dy, dx in {-1, 0, 1}, of
   // x * w[ci][co][k(ry, dy)][k(rx, dx)] with k(0, d) = 2 - 2d, k(1, d) = 3 - 2d (none for d = -1):
   // W'[ph][co][((dy+1)*3 + dx+1)*Cin + ci] (transposed-conv weight layout [Cin][Cout][5][5])
-  size_t pack_convt_subpix(const float* W, int Cout, int Cin) {
+  // centre_only (a 1x1 input grid, where the d = +-1 taps read only padding): the d = 0 tap alone,
+  // W'[ph][co][ci] (K = Cin, ksize 1, pad 0).
+  size_t pack_convt_subpix(const float* W, int Cout, int Cin, size_t* wfrag = nullptr, bool centre_only = false) {
     auto kk = [](int r, int d) { return r == 0 ? 2 - 2 * d : (d < 0 ? -1 : 3 - 2 * d); };
-    const int K = 9 * Cin;
+    const int rd = centre_only ? 0 : 1, kw = 2 * rd + 1, K = kw * kw * Cin;
     std::vector<float> tmp((size_t)4 * Cout * K, 0.f);
     for (int ph = 0; ph < 4; ++ph) {
       const int ry = ph >> 1, rx = ph & 1;
       for (int co = 0; co < Cout; ++co)
-        for (int dy = -1; dy <= 1; ++dy)
-          for (int dx = -1; dx <= 1; ++dx) {
+        for (int dy = -rd; dy <= rd; ++dy)
+          for (int dx = -rd; dx <= rd; ++dx) {
             const int ky = kk(ry, dy), kx = kk(rx, dx);
             if (ky < 0 || kx < 0 || !W) continue;
             for (int ci = 0; ci < Cin; ++ci)
-              tmp[((size_t)ph * Cout + co) * K + ((dy + 1) * 3 + dx + 1) * Cin + ci] =
+              tmp[((size_t)ph * Cout + co) * K + ((dy + rd) * kw + dx + rd) * Cin + ci] =
                   W[(((size_t)ci * Cout + co) * 5 + ky) * 5 + kx];
           }
     }
+    if (wfrag) *wfrag = frag4(tmp, Cout, K);
     if (u->bf16) {
       std::vector<uint16_t> b(tmp.size());
       for (size_t i = 0; i < tmp.size(); ++i) b[i] = host_f2bf(tmp[i]);
@@ -430,8 +438,10 @@ struct Builder {
     o.temb_col = temb_col; o.resid = resid;
     u->ops.push_back(o);
   }
+  // (Wx / bx: weights [Cout][Cin][ks][ks] and bias built by the caller instead of name's)
   int conv_layer(int s1, int s2, const std::string& name, int Cout, int ks, int stride, int pad, int ups, int Hout,
-                 int Wout, int temb_col = -1, int resid = -1, const std::string& gn = "") {
+                 int Wout, int temb_col = -1, int resid = -1, const std::string& gn = "", const float* Wx = nullptr,
+                 const float* bx = nullptr) {
     const int Cin = u->acts[s1].C + (s2 >= 0 ? u->acts[s2].C : 0);
     size_t coef = SIZE_MAX;
     if (!gn.empty()) {  // GN coefficient op feeding the fused conv
@@ -444,9 +454,31 @@ struct Builder {
       ws_off = (ws_off + (size_t)u->nb_max * Cin * 2 * 4 + 255) & ~(size_t)255;
       u->ops.push_back(g);
     }
-    const float* W = get(name + ".weight", (int64_t)Cout * Cin * ks * ks);
+    const float* W = Wx ? Wx : get(name + ".weight", (int64_t)Cout * Cin * ks * ks);
+    // Taps that read only padding for EVERY output pixel (the 1x1 / 2x2 levels of Arch C: a 3x3
+    // conv on a 1x1 image uses its centre tap alone; a stride-2 3x3 / 5x5 conv 2x2 -> 1x1 uses a
+    // 2x2 window) are dropped: the conv runs as the ks' x ks' window with pad' = pad - k0.
+    // Tap ky is live iff some output row reads an in-range input row:
+    // pad - (Hout-1)*stride <= ky <= Hin + pad - 1. Exact (the dropped taps multiply zeros).
+    std::vector<float> wwin;
+    {
+      const Act& A = u->acts[s1];
+      const int k0 = std::max(0, pad - (Hout - 1) * stride), k1 = std::min(ks - 1, A.H + pad - 1);
+      const int x0 = std::max(0, pad - (Wout - 1) * stride), x1 = std::min(ks - 1, A.W + pad - 1);
+      if (itsd::g_tap_prune && gn.empty() && !ups && W && (k0 > 0 || k1 < ks - 1) && k0 == x0 && k1 == x1 && k1 >= k0) {
+        const int ks2 = k1 - k0 + 1;
+        wwin.resize((size_t)Cout * Cin * ks2 * ks2);
+        for (size_t oc = 0; oc < (size_t)Cout * Cin; ++oc)
+          for (int ky = 0; ky < ks2; ++ky)
+            for (int kx = 0; kx < ks2; ++kx)
+              wwin[(oc * ks2 + ky) * ks2 + kx] = W[(oc * ks + k0 + ky) * ks + k0 + kx];
+        W = wwin.data();
+        ks = ks2;
+        pad -= k0;
+      }
+    }
     size_t wt = pack({W}, Cout, Cin, ks);
-    size_t b = f32(name + ".bias", Cout);
+    size_t b = bx ? ar.add(bx, (size_t)Cout * 4) : f32(name + ".bias", Cout);
     int dst = act(Hout, Wout, Cout);
     conv(s1, s2, dst, wt, b, Cout, ks, stride, pad, ups, temb_col, resid);
     u->ops.back().coef = coef;
@@ -617,9 +649,26 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
       const int Hc = b.u->acts[cur].H;
       if (!u->cfg) {
         cur = b.conv_layer(cur, -1, p + ".main", now, 3, 2, 1, 0, Hc / 2, Hc / 2);
-      } else {  // c1(x) + c2(x), ModelCondition.py:71-73
+      } else if (!itsd::g_down_merge) {  // c1(x) + c2(x), ModelCondition.py:71-73, as two convs
         int t1 = b.conv_layer(cur, -1, p + ".c1", now, 3, 2, 1, 0, Hc / 2, Hc / 2);
         cur = b.conv_layer(cur, -1, p + ".c2", now, 5, 2, 2, 0, Hc / 2, Hc / 2, -1, t1);
+      } else {  // c1(x) + c2(x), ModelCondition.py:71-73: both stride 2 and centred on the same input
+        // pixel (3x3 pad 1, 5x5 pad 2), so the sum is ONE 5x5 conv with c1's taps added onto c2's
+        // inner 3x3 (summed in fp32 before packing) and bias b1 + b2: 25 Cin of K instead of 34 Cin,
+        // one launch and no intermediate tensor
+        const int Cin = b.u->acts[cur].C;
+        const float* W1 = b.get(p + ".c1.weight", (int64_t)now * Cin * 9);
+        const float* W2 = b.get(p + ".c2.weight", (int64_t)now * Cin * 25);
+        const float* b1 = b.get(p + ".c1.bias", now);
+        const float* b2 = b.get(p + ".c2.bias", now);
+        std::vector<float> wm((size_t)now * Cin * 25, 0.f), bm(now, 0.f);
+        if (W2) std::memcpy(wm.data(), W2, wm.size() * 4);
+        if (W1)
+          for (size_t oc = 0; oc < (size_t)now * Cin; ++oc)
+            for (int ky = 0; ky < 3; ++ky)
+              for (int kx = 0; kx < 3; ++kx) wm[(oc * 5 + ky + 1) * 5 + kx + 1] += W1[(oc * 3 + ky) * 3 + kx];
+        for (int c = 0; c < now; ++c) bm[c] = (b1 ? b1[c] : 0.f) + (b2 ? b2[c] : 0.f);
+        cur = b.conv_layer(cur, -1, p + ".c12", now, 5, 2, 2, 0, Hc / 2, Hc / 2, -1, -1, "", wm.data(), bm.data());
       }
       hs.push_back(cur);
     }
@@ -651,10 +700,16 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
         if (((Hc * Hc) % 128 == 0 || 128 % (Hc * Hc) == 0) && now % (8 * epc) == 0) {
           // sub-pixel form: 4 phase-wise 3x3 convs over the input grid (9 of the 25 taps a phase,
           // against 25 per output of the zero-insertion form)
-          size_t wt = b.pack_convt_subpix(Wt, now, now);
+          // (+ the fragment-ordered phase weights for conv3x3_gn_p4_kernel's sub-pixel form at 8x8 .. 32x32 inputs)
+          size_t wf = SIZE_MAX;
+          const bool p4sub = now % 128 == 0 && now >= 128 && (Hc == 8 || Hc == 16 || Hc == 32);
+          // (a 1x1 input grid: the centre tap alone, K = Cin instead of 9 Cin)
+          const bool c1 = Hc == 1 && itsd::g_tap_prune;
+          size_t wt = b.pack_convt_subpix(Wt, now, now, p4sub ? &wf : nullptr, c1);
           if (Hc * Hc < 128) u->acts[tmp].spi = 4;  // one statistics slot per (image, phase)
-          b.conv(cur, -1, tmp, wt, bt, now, 3, 1, 1, 0);
+          b.conv(cur, -1, tmp, wt, bt, now, c1 ? 1 : 3, 1, c1 ? 0 : 1, 0);
           u->ops.back().subpix = 2;
+          u->ops.back().wfrag = wf;
         } else {
           size_t wt = b.pack({Wt}, now, now, 5, true);
           b.conv(cur, -1, tmp, wt, bt, now, 5, 1, 2, 0, -1, -1, 1);
@@ -823,7 +878,7 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
       a.subpix = o.subpix;
       a.Hout = in.H; a.Wout = in.W;
       a.M = c.nb * in.H * in.W;
-      a.ksize = o.subpix == 2 ? 3 : 2; a.pad = o.subpix == 2 ? 1 : 0; a.upsample = 0; a.zins = 0;
+      a.ksize = o.subpix == 2 ? o.ksize : 2; a.pad = o.subpix == 2 ? o.pad : 0; a.upsample = 0; a.zins = 0;
       a.K = a.ksize * a.ksize * (a.C1 + a.C2);
     }
     if (o.coef != SIZE_MAX) {
@@ -1218,6 +1273,14 @@ int itsd_set_option(const char* key, int value) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 6)
       return fail(ITSD_ERR_INVALID, "attn_split in {0, 1, 2, 4, 6}");
     itsd::g_attn_split = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "tap_prune")) {  // drop all-padding conv taps at build time (UNets created afterwards)
+    itsd::g_tap_prune = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "down_merge")) {  // CFG DownSample c1 + c2 as one 5x5 conv (UNets created afterwards)
+    itsd::g_down_merge = value ? 1 : 0;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards

@@ -119,7 +119,42 @@ __device__ __forceinline__ void mma_stage(const char* A, const char* B, f32x16 (
 // 3. per-channel (sum, sum of squares) over each pixel slot of the tile: the
 //    GroupNorm statistics of the consumer (Model.py:171,180), written as a
 //    deterministic partial slab stats[slot][2][Cout] (no atomics).
-template <typename T, int BM = 128, int BN = 128, int NTH = 256>
+// Additive values (bias + temb row + CFG cond row) of UB tile entries it0 + u * step (image
+// img0 + it / BM, cout tileC + it % BM), all loads of the batch issued before the first use: the
+// labels first, then the rows (the cond row's address depends on the label).
+template <int BM, int UB>
+__device__ __forceinline__ void addv_batch(const ConvArgs& a, int tileC, int img0, int HWo, int nent, long long trow,
+                                           int it0, int step, float (&v)[UB]) {
+  int lab[UB];
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    const int it = it0 + u * step, img = img0 + it / BM;
+    lab[u] = 0;
+    if (a.cemb && it < nent && (long long)img * HWo < a.M && (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from))
+      lab[u] = a.cemb_labels[img % a.cemb_label_mod];
+  }
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    const int it = it0 + u * step, co = tileC + it % BM, img = img0 + it / BM;
+    float x = 0.f;
+    if (it < nent && co < a.Cout && (long long)img * HWo < a.M) {
+      x = a.bias[co];
+      if (a.temb) x += a.temb[trow + (long long)img * a.temb_img_stride + co];
+      if (a.cemb) x += a.cemb[(long long)lab[u] * a.cemb_row_stride + co];
+    }
+    v[u] = x;
+  }
+}
+__device__ __forceinline__ long long temb_row_of(const ConvArgs& a) {
+  return a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
+}
+
+// ADDV: floats of LDS after the fp32 tile for the staged additive rows (EPI_BYTES: 16 images of 128
+// couts); a tile holding more images (the 2x2 / 1x1 levels: 32 / 128 images per 128-pixel tile)
+// reads its rows from global memory per output chunk instead.
+// PRE: the caller has already written the additive rows to LDS (E + BN * ER).
+template <typename T, int BM = 128, int BN = 128, int NTH = 256, int ADDV = (EPI_BYTES - 128 * EROW * 4) / 4,
+          bool PRE = false>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
 
 // accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
@@ -147,7 +182,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
 
 // E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
 // and the consumer GroupNorm's statistics slab.
-template <typename T, int BM, int BN, int NTH>
+template <typename T, int BM, int BN, int NTH, int ADDV, bool PRE>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int ER = BM + 4;  // E row (floats): 128x128 tile -> EROW
@@ -187,21 +222,20 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
   float* addv = E + BN * ER;  // [images of the tile][BM]
   const int img0 = tileP / HWo;
   const int nimt = HWo >= BN ? 1 : BN / HWo;
-  {
-    const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tid; it < nimt * BM; it += NT) {
-      const int il = it / BM, cl = it % BM, co = tileC + cl, img = img0 + il;
-      float v = 0.f;
-      if (co < a.Cout && (long long)img * HWo < a.M) {
-        v = a.bias[co];
-        if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
-        if (a.cemb) {
-          int lab = 0;
-          if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
-          v += a.cemb[(long long)lab * a.cemb_row_stride + co];
-        }
-      }
-      addv[it] = v;
+  const bool staged = nimt * BM <= ADDV;
+  const long long trow0 = temb_row_of(a);
+  if (staged && !PRE) {
+    // 8 entries per thread per batch, every load of a batch issued before the first use (the
+    // CFG model's 2x2 / 1x1 tiles hold 32 / 64 images: one dependent label -> cond-row round trip
+    // per entry in a plain loop was ~12 us of a ~15 us conv)
+    constexpr int UB = 8;
+    const int nent = nimt * BM;
+    for (int it0 = tid; it0 < nent; it0 += UB * NT) {
+      float v[UB];
+      addv_batch<BM, UB>(a, tileC, img0, HWo, nent, trow0, it0, NT, v);
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+        if (it0 + u * NT < nent) addv[it0 + u * NT] = v[u];
     }
   }
   constexpr int CPR = BM / EPC;  // 16-B output chunks per tile row
@@ -226,14 +260,29 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
     const int pl = tid / CPR + k * RPI;
     const int p = tileP + pl;
     if (pl >= BN || p >= a.M || co >= a.Cout) continue;
-    const float* av = addv + (HWo >= BN ? 0 : pl / HWo) * BM + cl;
     float v[EPC];
+    if (staged) {
+      const float* av = addv + (HWo >= BN ? 0 : pl / HWo) * BM + cl;
 #pragma unroll
-    for (int q = 0; q < EPC / 4; ++q) {
-      const f32x4 e4 = *(const f32x4*)(E + pl * ER + cl + 4 * q);
-      const f32x4 b4 = *(const f32x4*)(av + 4 * q);
+      for (int q = 0; q < EPC / 4; ++q) {
+        const f32x4 e4 = *(const f32x4*)(E + pl * ER + cl + 4 * q);
+        const f32x4 b4 = *(const f32x4*)(av + 4 * q);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
+      }
+    } else {  // the chunk's EPC additive values straight from the bias / temb / cond rows
+      const int img = p / HWo;
+      int lab = 0;
+      if (a.cemb && (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from)) lab = a.cemb_labels[img % a.cemb_label_mod];
+#pragma unroll
+      for (int q = 0; q < EPC / 4; ++q) {
+        const f32x4 e4 = *(const f32x4*)(E + pl * ER + cl + 4 * q);
+        f32x4 b4 = *(const f32x4*)(a.bias + co + 4 * q);
+        if (a.temb) b4 += *(const f32x4*)(a.temb + trow0 + (long long)img * a.temb_img_stride + co + 4 * q);
+        if (a.cemb) b4 += *(const f32x4*)(a.cemb + (long long)lab * a.cemb_row_stride + co + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] = e4[e] + b4[e];
+      }
     }
     if (a.resid) {
       const T* re = (const T*)&rres[k];
@@ -630,6 +679,22 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       }
     tmask[q] = m;
   }
+  // the tile's additive rows (<= 64 images x 64 couts: <= 16 entries a thread), loaded before the K
+  // loop so their label -> cond-row round trips overlap it (the 2x2 / 1x1 levels' tiles hold 16-64
+  // images); written to LDS after the loop (epilogue_from_E<..., PRE>)
+  float pre[16];
+  {
+    const int nent = (HWo >= SM_B ? 1 : SM_B / HWo) * SM_B;
+    const long long trow = temb_row_of(a);
+    float v0[8], v1[8];
+    addv_batch<SM_B, 8>(a, tileC, tileP / HWo, HWo, nent, trow, tid, 256, v0);
+    addv_batch<SM_B, 8>(a, tileC, tileP / HWo, HWo, nent, trow, tid + 2048, 256, v1);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      pre[u] = v0[u];
+      pre[8 + u] = v1[u];
+    }
+  }
   const int ntap = a.ksize * a.ksize;
   const int S = gridDim.z, kc0 = bt.z * nK / S, nKs = (bt.z + 1) * nK / S - kc0;
   auto issue = [&](int kc, int slot) {
@@ -726,15 +791,22 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
     }
     __syncthreads();  // flag read by every wave before E overwrites it
   }
-  // accumulators -> E[pixel][cout] (row SM_B + 4 floats)
+  // accumulators -> E[pixel][cout] (row SM_B + 4 floats); the additive rows after it
   float* E = (float*)smem;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     f32x4 v4 = {acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
     *(f32x4*)(E + (wn * 32 + rl) * (SM_B + 4) + wm * 32 + 8 * g + 4 * hh) = v4;
   }
+  {
+    const int nent = (HWo >= SM_B ? 1 : SM_B / HWo) * SM_B;
+    float* addv = E + SM_B * (SM_B + 4);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (tid + 256 * u < nent) addv[tid + 256 * u] = pre[u];
+  }
   __syncthreads();
-  epilogue_from_E<T, SM_B, SM_B>(a, smem, tileP, tileC, -1);
+  epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true>(a, smem, tileP, tileC, -1);
 }
 
 // Host-side eligibility of conv_small (bf16, whole 128-B K-chunks, plain stride/pad addressing).
@@ -1230,17 +1302,19 @@ constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 M
 // (W = 32, 16) only. The halo waves are the same.
 constexpr int P16_RING = 2;  // A k32-step slots (divides the 18 k32-steps of a chunk)
 // AB: bit 1 (value 2) = plain conv3x3 (no GroupNorm+SiLU: the halo waves copy the input; shipped, the
-// CFG UpSample's 3x3 conv, conv_p4_plain_selected); bit 7 (value 128) = the sub-pixel form of a
-// nearest-x2 upsample + conv3x3 (Model.py:121-126; plain): W is the INPUT grid, a tile is (phase, 256
-// input-grid pixels, 128 couts), 4 taps (the phase's 2x2 folded weights, wfrag [4 phases][Cout/32][K/16])
-// at halo offsets (dy + py, dx + px), outputs scattered to (2i + py, 2j + px) and the statistics slots of
-// each (image, phase) (conv_p4_sub_selected); the other bits are diagnostic
-// ablations (ITSD_DIAG).
+// CFG UpSample's 3x3 conv, conv_p4_plain_selected); bit 7 (value 128) = a sub-pixel phase conv (plain):
+// W is the INPUT grid, a tile is (phase, 256 input-grid pixels, 128 couts) with the phase's weights
+// (wfrag [4 phases][Cout/32][K/16]), outputs scattered to (2i + py, 2j + px) of the 2x grid and the
+// statistics slots of each (image, phase) -- 4 taps at halo offsets (dy + py, dx + px) for a nearest-x2
+// upsample + conv3x3 (Model.py:121-126, the phase's 2x2 folded taps), or with bit 8 (value 256) the 9
+// taps of a 3x3 window for ConvTranspose2d(5, 2, 2, 1) (ModelCondition.py:80, the phase's taps of the 5x5
+// kernel) (conv_p4_sub_selected); the other bits are diagnostic ablations (ITSD_DIAG).
 template <int W, int AB = 0, bool M16 = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   typedef bf16_t T;
   constexpr bool SUB = (AB & 128) != 0, PLAIN = SUB || (AB & 2) != 0;
-  constexpr int NTAP = SUB ? 4 : 9, KST = 4 * NTAP;  // taps and 16-deep k-steps of a 64-channel chunk
+  constexpr bool SUB4 = SUB && (AB & 256) == 0;      // upsample phases: 2x2 taps; else 3x3 windows
+  constexpr int NTAP = SUB4 ? 4 : 9, KST = 4 * NTAP;  // taps and 16-deep k-steps of a 64-channel chunk
   constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = GnpCfg<W>::ITEMS, RES = GnpCfg<W>::RES;
   constexpr int W2 = W + 2;
   constexpr int THs = NSEG == 1 ? GNW_BN / W : W;
@@ -1249,7 +1323,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  constexpr int RING = (AB & 64) ? 4 : (SUB ? 4 : P4_RING), BD = (AB & 32) ? P4_BD + 1 : P4_BD;
+  constexpr int RING = (AB & 64) ? 4 : (SUB4 ? 4 : P4_RING), BD = (AB & 32) ? P4_BD + 1 : P4_BD;
   static_assert(KST % RING == 0, "ring slots repeat per chunk");
   static_assert(!(SUB && M16), "the sub-pixel form runs the 32x32x16 MFMA path");
   // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]
@@ -1528,8 +1602,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         auto rd = [&](int st, int buf) __attribute__((always_inline)) {
           if ((st & 3) == 0) {
             const int tap = st >> 2;
-            // SUB: tap (dy, dx) of phase (py, px) reads input offset (dy + py - 1, dx + px - 1)
-            const int ky = SUB ? (tap >> 1) + (tph >> 1) : tap / 3, kx = SUB ? (tap & 1) + (tph & 1) : tap - (tap / 3) * 3;
+            // SUB4: tap (dy, dx) of phase (py, px) reads input offset (dy + py - 1, dx + px - 1)
+            const int ky = SUB4 ? (tap >> 1) + (tph >> 1) : tap / 3, kx = SUB4 ? (tap & 1) + (tph & 1) : tap - (tap / 3) * 3;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               int h = hb[j] + ky * W2 + kx;
@@ -2939,12 +3013,14 @@ bool conv_p4_plain_selected(const ConvArgs& a) {
          (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
 }
 
-// A nearest-x2 upsample conv (sub-pixel phases, subpix 1) on conv3x3_gn_p4_kernel<W, 128>? W = the input
-// grid (8 / 16 / 32); auto where the 4 phases x 256-pixel tiles x 128-cout tiles fill the chip (>= 192)
+// A sub-pixel phase conv on conv3x3_gn_p4_kernel<W, 128 | 256 x (ConvTranspose2d)>? subpix 1: the 2x2-tap
+// phases of a nearest-x2 upsample conv; subpix 2: the 3x3-tap phases of ConvTranspose2d(5, 2, 2, 1). W = the
+// input grid (8 / 16 / 32); auto where the 4 phases x 256-pixel tiles x 128-cout tiles fill the chip (>= 192)
 bool conv_p4_sub_selected(const ConvArgs& a) {
-  if (!g_p4_sub || a.subpix != 1 || !a.wfrag || a.ksize != 2 || a.resid || a.vt_out || !a.zero || a.gn_coef ||
-      a.Hout != a.Wout || !(a.Wout == 8 || a.Wout == 16 || a.Wout == 32) || a.Cout % CONV_BM || a.C1 % 64 ||
-      a.C2 % 64 || a.C1 + a.C2 < 128 || a.K != 4 * (a.C1 + a.C2) || a.M % GNW_BN)
+  const int taps = a.subpix == 1 ? 4 : 9;
+  if (!g_p4_sub || !a.subpix || !a.wfrag || a.ksize * a.ksize != taps || a.resid || a.vt_out || !a.zero ||
+      a.gn_coef || a.Hout != a.Wout || !(a.Wout == 8 || a.Wout == 16 || a.Wout == 32) || a.Cout % CONV_BM ||
+      a.C1 % 64 || a.C2 % 64 || a.C1 + a.C2 < 128 || a.K != taps * (a.C1 + a.C2) || a.M % GNW_BN)
     return false;
   return 4LL * (a.M / GNW_BN) * (a.Cout / CONV_BM) >= 192;
 }
@@ -3063,14 +3139,21 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   const int v = g_conv_variant;
   const bool lin = !(a.upsample | a.zins);
   if (a.subpix) {
-    if (!pipe || !lin || a.ksize != (a.subpix == 2 ? 3 : 2) || ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
+    if (!pipe || !lin || (a.subpix == 2 ? (a.ksize != 3 && !(a.ksize == 1 && a.Hout * a.Wout == 1)) : a.ksize != 2) ||
+        ((a.Hout * a.Wout) % 128 && 128 % (a.Hout * a.Wout)))
       return hipErrorInvalidValue;
     if constexpr (sizeof(T) == 2) {
       if (conv_p4_sub_selected(a)) {  // 4 phases x pixel tiles x cout tiles, persistent
         const dim3 gp(std::min(4 * (a.M / GNW_BN) * (a.Cout / CONV_BM), g_num_cus));
-        if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 128>), gp, dim3(512), 0, s, a);
-        else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 128>), gp, dim3(512), 0, s, a);
-        else ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 128>), gp, dim3(512), 0, s, a);
+        if (a.subpix == 1) {
+          if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 128>), gp, dim3(512), 0, s, a);
+          else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 128>), gp, dim3(512), 0, s, a);
+          else ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 128>), gp, dim3(512), 0, s, a);
+        } else {
+          if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 384>), gp, dim3(512), 0, s, a);
+          else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 384>), gp, dim3(512), 0, s, a);
+          else ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 384>), gp, dim3(512), 0, s, a);
+        }
         return hipGetLastError();
       }
     }

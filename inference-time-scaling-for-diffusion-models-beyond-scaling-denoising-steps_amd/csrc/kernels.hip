@@ -723,13 +723,13 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 // Hand-offs: MI355X_MICROARCH.md visibility table, row 1 (sc1 stores; every storing wave waits
 // vmcnt(0); a workgroup barrier; one agent-scope atomic add per block; one lane polls with sc1 loads
 // (s_sleep, bounded); a workgroup barrier; every load of the handed-off bytes an sc1 load). The counters
-// only grow: a block's target is (old / G + 1) * G from the value its own add returned (launches on a
-// stream never overlap). Waiting blocks need the whole grid resident: the host launches it only when
+// only grow, by 12 per launch (12 / G per block), so a block's target -- the next multiple of 12 above the
+// value its own add returned -- holds whatever G earlier launches used (launches on a stream never overlap). Waiting blocks need the whole grid resident: the host launches it only when
 // n * G <= CUs (one 512-thread block per CU).
 template <int C, int G>
 __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs a) {
   constexpr int S = 64, KS = C / 16, CB = C / 32, CBg = CB / G, CW = CBg * 32, PF = 8;
-  static_assert(CB % G == 0 && C % 128 == 0, "G divides the channel blocks");
+  static_assert(CB % G == 0 && C % 128 == 0 && 12 % G == 0, "G divides the channel blocks and 12");
   constexpr int QROW = CW * 2 + 16;  // Q_g / K_g row (bytes): padded so 16-B reads of 16 rows are conflict-free
   constexpr int R_VT = S * C * 2, R_Q = R_VT + CW * 128, R_K = R_Q + S * QROW, R_SM = R_K + S * QROW;
   constexpr int R_PM = R_SM + S * (S + 4) * 4, R_GS = R_PM + S * 128, R_ST = R_GS + 32 * 2 * 4;
@@ -743,6 +743,18 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   auto frag = [&](const bf16_t* W, int cb, int st) -> const bf16x8* {
     return (const bf16x8*)((const char*)W + ((size_t)cb * KS + st) * 1024 + lane * 16);
   };
+  // projection unit u = kind * CBg + cbl (kind 0 V, 1 Q, 2 K): its fragment row of the packed q|k|v matrix
+  auto frow_of = [&](int u) {
+    const int kind = u / CBg, cb = g * CBg + u - kind * CBg;
+    return kind == 0 ? 2 * CB + cb : (kind - 1) * CB + cb;
+  };
+  // the first PF weight fragments of this wave's first unit, in flight before anything else (they depend
+  // on no earlier kernel: their latency hides behind the x loads and the GroupNorm)
+  bf16x8 fw[PF];
+  if (w < 3 * CBg) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) fw[p] = *frag(a.wqkv, frow_of(w), p);
+  }
   // ---- 0. GroupNorm statistics and hn (attn_block_kernel's phase 0)
   constexpr int XU = S * (C / 8) / 512;
   u32x4 xv[XU];
@@ -796,16 +808,14 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   }
   __syncthreads();
   auto hn_frag = [&](int r, int st) { return *(const bf16x8*)(sm + rowc(r, 2 * st + hh, C * 2)); };
-  // weight-stream unit: one 32-channel block of a projection over both token blocks (fragments loaded once)
+  // weight-stream unit: one 32-channel block of a projection over both token blocks (fragments loaded once);
+  // fw holds the unit's first PF fragments when it is called
   auto unit = [&](const bf16_t* W, int frow, f32x16 (&acc)[2], auto vform) __attribute__((always_inline)) {
     constexpr bool VF = decltype(vform)::value;  // true: D[token][c] (A = hn); false: D[c][token] (A = W)
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[tb][r] = 0.f;
-    bf16x8 fw[PF];
-#pragma unroll
-    for (int p = 0; p < PF; ++p) fw[p] = *frag(W, frow, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       const bf16x8 cur = fw[st % PF];
@@ -822,6 +832,10 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   for (int u = w; u < 3 * CBg; u += 8) {
     const int kind = u / CBg, cbl = u - kind * CBg, cb = g * CBg + cbl;
     f32x16 acc[2];
+    if (u != w) {  // a wave's later units (G <= 4): their first fragments now
+#pragma unroll
+      for (int p = 0; p < PF; ++p) fw[p] = *frag(a.wqkv, frow_of(u), p);
+    }
     if (kind == 0) {
       unit(a.wqkv, 2 * CB + cb, acc, std::true_type{});
       // lane: channel 32 cb + rl, tokens 32 tb + 8 q + 4 hh + e -> V^T row (local channel), 4 tokens a store
@@ -870,12 +884,16 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
                                              sp, off + q * 16, 0, 16);
   }
   // hand-off: this block's stores drained, one add, one lane polls until the image's G blocks have added
-  auto handoff = [&](int* cnt) __attribute__((always_inline)) {
+  // Every launch adds exactly 12 to each counter (12 / G per block; G in {2, 4, 6}), so between launches a
+  // counter is a multiple of 12 whatever G earlier launches used, and a block's target is the next one.
+  // `during` runs between the barriers while lane 0 of wave 0 polls (work that needs no handed-off byte)
+  auto handoff = [&](int* cnt, auto during) __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    during();
     if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int target = (old / G + 1) * G;
+      const int old = __hip_atomic_fetch_add(cnt, 12 / G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int target = (old / 12 + 1) * 12;
       for (int it = 0; it < (1 << 22); ++it) {  // bounded: a grid that is not co-resident cannot hang the GPU
         if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
         __builtin_amdgcn_s_sleep(2);
@@ -883,7 +901,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
     }
     __syncthreads();
   };
-  handoff(a.sync + 2 * img);
+  handoff(a.sync + 2 * img, [] {});
   // every block: S = sum of the G partials in g order (waves 0..3, their tile), scaled -> Sm [query][key]
   float* const Sm = (float*)(sm + R_SM);
   char* const Pm = sm + R_PM;
@@ -955,7 +973,13 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
                                             osl, (uint32_t)((((size_t)img * S + q) * C + c) * 2), 0, 16);
     }
   }
-  handoff(a.sync + 2 * img + 1);
+  // (the proj unit's first fragments go out while the block waits for the other slices)
+  handoff(a.sync + 2 * img + 1, [&] {
+    if (w < CBg) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) fw[p] = *frag(a.wp, g * CBg + w, p);
+    }
+  });
   // the full O [token][C] (every block's slice) -> hn's rows (hn is dead since phase 1)
   for (int i = tid; i < S * (C / 8); i += 512) {
     const int t = i / (C / 8), ch = i - t * (C / 8);
@@ -966,7 +990,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   // ---- 4. out = x + O Wp^T + bp for this block's output channels; statistics of its channels
   float* const spart = (float*)(sm + R_ST);  // [token block][2][CW]
   bf16_t* out = a.out + (size_t)img * S * C;
-  for (int cbl = w; cbl < CBg; cbl += 8) {
+  for (int cbl = w; cbl < CBg; cbl += 8) {  // (CBg <= 6: one unit a wave, its fragments loaded above)
     const int cb = g * CBg + cbl;
     f32x16 acc[2];
     unit(a.wp, cb, acc, std::false_type{});  // D[c'][token]
@@ -1079,32 +1103,41 @@ bool attn_block_ok(int S, int C) { return S == 64 && (C == 128 || C == 256 || C 
 
 // Flash-style MFMA attention for long sequences (S > 256: the CFG UNet's 32x32 level,
 // S = 1024, C = 128, ModelCondition.py:98-118; Arch A at 64/256 px). No S x S tile is
-// materialised: each wave owns 32 queries and streams 32-key tiles with an online softmax.
-//  - scores are computed transposed, s^T = K q^T (A = 32 keys x 16 ch from the q|k|v rows,
-//    B = q^T), so every lane holds 16 keys of ONE query: the row max / row sum is a
-//    register reduction plus one xor-32 shuffle, and the rescale of O is one factor/lane;
-//  - O^T = V^T P^T with P^T straight from the score registers (bf16): the MFMA B operand
-//    of lane (query, hi) is its 8 score registers r = 8j..8j+7, i.e. keys
-//    {16j+4hi+0..3, 16j+8+4hi+0..3}; the A operand (V^T, channel-major from the qkv conv
-//    epilogue) is read with the same key permutation (two 8-B loads per lane), so the
-//    contraction over keys is exact without any register shuffle.
+// materialised: each wave owns 32 queries, and the block's 4 waves (128 queries) stream
+// 32-key tiles of K and V^T through LDS with an online softmax.
+//  - K / V^T tiles are double-buffered in LDS with one barrier a tile (the next tile's global
+//    loads are in flight while the current one is consumed): each K / V byte is fetched from
+//    L2 once per block, not once per wave (the per-wave form was bound by those loads);
+//  - blocks run XCD-major (block b on XCD b % 8 takes logical tile (b % 8) * nb/8 + b / 8), so the
+//    query tiles of one image share one XCD's L2 for that image's K / V;
+//  - scores are computed transposed, s^T = K q^T (A = 32 keys x 16 ch, B = q^T), so every lane
+//    holds 16 keys of ONE query: the row max / row sum is a register reduction plus one xor-32
+//    shuffle, and the rescale of O is one factor/lane;
+//  - O^T = V^T P^T with P^T straight from the score registers (bf16): the MFMA B operand of lane
+//    (query, hi) is its 8 score registers r = 8j..8j+7, i.e. keys {16j+4hi+0..3, 16j+8+4hi+0..3};
+//    V^T rows sit in LDS with each 16-key group stored in the order 0-3, 8-11, 4-7, 12-15, so the
+//    A operand of lane (channel, hi) is ONE 16-byte LDS read at position 16j + 8hi.
 // CB = C / 32 channel blocks (C <= 256: q fragment and O accumulators stay in registers).
 template <int CB>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
-  constexpr int C = CB * 32, C3 = 3 * C, QS = C / 16;
-  const int S = a.S;
-  const int img = blockIdx.y;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, rl = lane & 31, hh = lane >> 5;
-  const int q = blockIdx.x * 128 + wid * 32 + rl;
+  constexpr int C = CB * 32, C3 = 3 * C, QS = C / 16, KP = C + 8, VP = 40, NSEG = CB / 2;
+  static_assert(CB % 2 == 0, "two 16-byte segments of K and of V^T per thread per 64 channels");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][32 * KP];  // [key][channel] (+8 pad)
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][C * VP];   // [channel][permuted key] (+8 pad)
+  const int S = a.S, QT = (S + 127) / 128;
+  const int nb = gridDim.x, bx = blockIdx.x;
+  const int L = (nb & 7) ? bx : (bx & 7) * (nb >> 3) + (bx >> 3);
+  const int img = L / QT, qt = L - img * QT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int q = qt * 128 + wid * 32 + rl;
   const bool qv = q < S;
   const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
   const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
-  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  bf16x8 qf[QS];
+  bf16x8 qf[QS];  // (a query past S reads row 0; its output is not stored)
   {
     const bf16_t* qp = base + (size_t)(qv ? q : 0) * C3 + 8 * hh;
 #pragma unroll
-    for (int i = 0; i < QS; ++i) qf[i] = qv ? *(const bf16x8*)(qp + 16 * i) : z8;
+    for (int i = 0; i < QS; ++i) qf[i] = *(const bf16x8*)(qp + 16 * i);
   }
   f32x16 o[CB];
 #pragma unroll
@@ -1113,29 +1146,43 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[cb][r] = 0.f;
   const float sl2 = a.scale * 1.4426950408889634f;  // softmax via exp2
   float m = -INFINITY, l = 0.f;
-  // K fragments one key tile ahead (their load latency behind the previous tile's softmax and PV)
-  bf16x8 kf[QS];
-  auto load_k = [&](int kt) {
-    const int key = kt + rl;
-    const bool kv = key < S;
-    const bf16_t* kp = base + (size_t)(kv ? key : 0) * C3 + C + 8 * hh;
-#pragma unroll
-    for (int i = 0; i < QS; ++i) kf[i] = kv ? *(const bf16x8*)(kp + 16 * i) : z8;
-  };
-  load_k(0);
-  for (int kt = 0; kt < S; kt += 32) {
+  // staging: thread tid moves 16-byte segments g = tid + 256 r of the K tile (key g / (C/8),
+  // channels 8 (g % (C/8)) ..) and of the V^T tile (channel g / 4, keys 8 (g % 4) ..); S % 8 == 0
+  // (S % 32 == 0, attn_flash_ok: every key of every tile exists, no masks)
+  u32x4 kr[NSEG], vr[NSEG];
+#define ITSD_FLASH_GLOAD(kt)                                                                 \
+  _Pragma("unroll") for (int r = 0; r < NSEG; ++r) {                                         \
+    const int g = tid + 256 * r;                                                             \
+    kr[r] = *(const u32x4*)(base + (size_t)((kt) + g / (C / 8)) * C3 + C + 8 * (g % (C / 8))); \
+    vr[r] = *(const u32x4*)(vt + (size_t)(g >> 2) * S + (kt) + 8 * (g & 3));                 \
+  }
+#define ITSD_FLASH_LSTORE(buf)                                                               \
+  _Pragma("unroll") for (int r = 0; r < NSEG; ++r) {                                         \
+    const int g = tid + 256 * r, sg = g & 3;                                                 \
+    *(u32x4*)&Ks[buf][(g / (C / 8)) * KP + 8 * (g % (C / 8))] = kr[r];                       \
+    bf16_t* vp = &Vs[buf][(g >> 2) * VP + 16 * (sg >> 1) + 4 * (sg & 1)];                    \
+    *(uint2*)vp = make_uint2(vr[r][0], vr[r][1]);       /* keys 8sg+0..3 */                    \
+    *(uint2*)(vp + 8) = make_uint2(vr[r][2], vr[r][3]); /* keys 8sg+4..7 */                    \
+  }
+  ITSD_FLASH_GLOAD(0)
+  ITSD_FLASH_LSTORE(0)
+  __syncthreads();
+  const int nt = (S + 31) / 32;
+  for (int t = 0; t < nt; ++t) {
+    const int kt = t * 32, buf = t & 1;
+    if (t + 1 < nt) { ITSD_FLASH_GLOAD(kt + 32) }
+    const bf16_t* ks = Ks[buf] + rl * KP + 8 * hh;
     f32x16 s;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
-    for (int i = 0; i < QS; ++i) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], s, 0, 0, 0);
-    if (kt + 32 < S) load_k(kt + 32);
+    for (int i = 0; i < QS; ++i)
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(ks + 16 * i), qf[i], s, 0, 0, 0);
     // s[r] = score(query rl, key kt + (r&3) + 8(r>>2) + 4hh) (unscaled)
     float mx = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int kk = kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      s[r] = kk < S ? s[r] * sl2 : -INFINITY;
+      s[r] *= sl2;
       mx = fmaxf(mx, s[r]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -1154,22 +1201,19 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
     for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+    const bf16_t* vs = Vs[buf] + rl * VP + 8 * hh;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       bf16x8 bp;
 #pragma unroll
       for (int i = 0; i < 8; ++i) bp[i] = (short)f2bf(s[8 * j + i]);
-      const int k0 = kt + 16 * j + 4 * hh;  // keys k0..k0+3 and k0+8..k0+11 (S % 8 == 0)
-      const bool v0 = k0 < S, v1 = k0 + 8 < S;
 #pragma unroll
-      for (int cb = 0; cb < CB; ++cb) {
-        const bf16_t* vp = vt + (size_t)(cb * 32 + rl) * S;
-        uint2 lo = v0 ? *(const uint2*)(vp + k0) : make_uint2(0, 0);
-        uint2 hi = v1 ? *(const uint2*)(vp + k0 + 8) : make_uint2(0, 0);
-        u32x4 w = {lo.x, lo.y, hi.x, hi.y};
-        o[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), bp, o[cb], 0, 0, 0);
-      }
+      for (int cb = 0; cb < CB; ++cb)
+        o[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(vs + cb * 32 * VP + 16 * j), bp, o[cb], 0,
+                                                        0, 0);
     }
+    if (t + 1 < nt) { ITSD_FLASH_LSTORE(buf ^ 1) }  // (buf ^ 1 was last read in tile t - 1, before the barrier)
+    __syncthreads();
   }
   if (!qv) return;
   const float inv = 1.0f / l;
@@ -1184,9 +1228,11 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
       w2.y = (uint32_t)f2bf(o[cb][4 * g + 2] * inv) | ((uint32_t)f2bf(o[cb][4 * g + 3] * inv) << 16);
       *(uint2*)(out + c) = w2;
     }
+#undef ITSD_FLASH_GLOAD
+#undef ITSD_FLASH_LSTORE
 }
 
-bool attn_flash_ok(int S, int C) { return S % 8 == 0 && (C == 64 || C == 128 || C == 256); }
+bool attn_flash_ok(int S, int C) { return S % 32 == 0 && (C == 64 || C == 128 || C == 256); }
 
 size_t attn_mfma_smem(int S) {
   const int Sp = (S + 31) & ~31;
@@ -1198,7 +1244,7 @@ hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (a.vt && a.S > 256) {
       if (!attn_flash_ok(a.S, a.C)) return hipErrorInvalidValue;
-      const dim3 grid((a.S + 127) / 128, n);
+      const dim3 grid((unsigned)(((a.S + 127) / 128) * n));
       if (a.C == 64) ITSD_LAUNCH(attn_flash_kernel<2>, grid, dim3(256), 0, s, a);
       else if (a.C == 128) ITSD_LAUNCH(attn_flash_kernel<4>, grid, dim3(256), 0, s, a);
       else ITSD_LAUNCH(attn_flash_kernel<8>, grid, dim3(256), 0, s, a);

@@ -13,11 +13,13 @@ C1 runs' 3 images and 3 of the 256 candidates (indices 0, 129, 255) in ONE batch
 fed its own counter-based noise (``R.philox_normal``: the seed the run used, the image's global
 element offset), so every comparison is one image's whole trajectory.
 
-Tolerances (measured values are printed):
-  C1 fp32 x0 (the saved image x0 * 0.5 + 0.5)      max|d| <= FULL_T_FP32_MAXABS
-  C2 bf16 x0 vs the fp32 oracle                    per-image rel-L2 <= FULL_T_BF16_REL_L2
-  C2 per-candidate Oracle-verifier score           |d| <= FULL_T_BF16_SCORE (the quantity the
-                                                   search prunes on)
+Tolerances (measured values are printed; first measurement, r04a):
+  C1 fp32 x0 (the saved image x0 * 0.5 + 0.5)      max|d| <= 5e-4    (measured 5.6e-5 / 9.4e-5)
+  C2 bf16 x0 vs the fp32 oracle                    rel-L2 <= 5e-2    (measured 3.0-3.4e-2: bf16 eps
+                                                   rounding compounds over 1000 steps; single pixels
+                                                   differ by up to ~1.5 at t = 0)
+  C2 per-candidate Oracle-verifier score           |d| <= 1e-3      (measured 1.9e-5 .. 1.1e-4: the
+                                                   quantity the search prunes on)
 """
 import numpy as np
 import pytest
@@ -34,9 +36,9 @@ from itsd.weights import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 
-FULL_T_FP32_MAXABS = 2e-3
+FULL_T_FP32_MAXABS = 5e-4
 FULL_T_BF16_REL_L2 = 5e-2
-FULL_T_BF16_SCORE = 5e-3
+FULL_T_BF16_SCORE = 1e-3
 
 T = 1000
 PER = 3 * 32 * 32

@@ -438,6 +438,77 @@ def test_p4_subpixel_upsample_convs_vs_conv_pipe_and_oracle(n):
     assert d < 1e-2 and e < REL_L2_BF16
 
 
+def test_p4_subpixel_convtranspose_vs_conv_pipe_cfg():
+    """The CFG UpSample's ConvTranspose2d(5, 2, 2, 1) (ModelCondition.py:80) as 4 sub-pixel phases of 3x3
+    taps on conv3x3_gn_p4_kernel (AB = 384: 16x16 -> 32x32 and 8x8 -> 16x16 inputs) against the same phase
+    GEMMs on conv_pipe (p4_sub = 0) at C3's guided batch (2N = 64): within 1e-2 relative L2, deterministic,
+    and the forward within the bf16 bound of the oracle."""
+    a = ARCH_C
+    net = _net(a, "bf16")
+    n = 64
+    gen = torch.Generator().manual_seed(640)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, a.T, (n,), generator=gen)
+    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n // 2, dtype=torch.long)])
+    x, t, lb = xc.cuda(), tc.cuda(), lab.cuda()
+    ops = net.native(n).profile_ops(x, t.to(torch.int32))
+    convt = [o["kernel"] for o in ops if "384>" in o["kernel"]]
+    assert any("conv3x3_gn_p4_kernel<16, 384>" in k for k in convt) and any("<8, 384>" in k for k in convt), convt
+
+    def run(**opts):
+        try:
+            for k, v in opts.items():
+                rt.set_option(k, v)
+            return net(x, t, lb).float().cpu()
+        finally:
+            rt.set_option("p4_sub", 1)
+
+    sub = run()
+    assert torch.equal(sub, run())
+    pipe = run(p4_sub=0)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
+    d, e = _rel_l2(sub, pipe), _rel_l2(sub[idx], ref)
+    print(f"CFG 2N=64: p4 sub-pixel ConvTranspose vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_dead_tap_pruning_archC_1x1_level(precision):
+    """Arch C's 1x1 level (ModelCondition.py: ch_mult [1, 4, 8, 8, 4, 2] at 32 px): taps that read only
+    padding for every output pixel are dropped at build time -- the 3x3 convs on 1x1 images run their
+    centre tap (ks 1), the DownSample 2x2 -> 1x1 (c1 3x3 + c2 5x5, stride 2, merged into one 5x5 conv at
+    build time) a 2x2 window, the ConvTranspose
+    from the 1x1 grid its centre tap per phase. Exact in arithmetic (the dropped taps multiply zero
+    padding): the census shows no 3x3+ conv left at H = 1, and a guided batch (2N = 64, the C3 leg's)
+    matches the oracle (fp32 max|d| <= 2e-4, bf16 rel-L2 <= 2e-2)."""
+    a = ARCH_C
+    net = _net(a, precision)
+    n = 64
+    gen = torch.Generator().manual_seed(641)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, a.T, (n,), generator=gen)
+    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n // 2, dtype=torch.long)])
+    x, t, lb = xc.cuda(), tc.cuda(), lab.cuda()
+    ops = net.native(n).profile_ops(x, t.to(torch.int32))
+    h1 = [o for o in ops if o["kind"] == "conv" and o["H"] == 1]
+    assert h1 and all(o["ks"] <= 2 for o in h1), [(o["ks"], o["K"], o["kernel"]) for o in h1]
+    assert sum(o["ks"] == 2 for o in h1) == 1  # the DownSample into the 1x1 level (c1 + c2 as one 5x5 s2 conv)
+    eps = net(x, t, lb).float().cpu()
+    idx = [0, 31, 32, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
+    if precision == "fp32":
+        d = (eps[idx] - ref).abs().max().item()
+        print(f"Arch C 2N=64 fp32 (pruned taps) max|d| vs oracle {d:.2e}")
+        assert d <= EPS_TOL_FP32
+    else:
+        e = _rel_l2(eps[idx], ref)
+        print(f"Arch C 2N=64 bf16 (pruned taps, LDS-staged flash attention) rel-L2 vs oracle {e:.2e}")
+        assert e < REL_L2_BF16
+
+
 def test_forward_bf16_full_batch_vs_oracle_subset():
     """The bench batch (N=256) runs the persistent fused convs with several tiles per block
     (4 at 32x32, 2 at 16x16), the 2-blocks-per-image attention grid and the split-K small level: images

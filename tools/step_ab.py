@@ -50,7 +50,8 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
             res[v].append(ms)
             for k in opts:  # back to the default of each option touched
-                rt.set_option(k, {"gn_fold": 1, "p5": 1, "p5_split": 0, "splitk_inl": 1, "p4_plain": 1, "splitk": 1}.get(k, 0))
+                rt.set_option(k, {"gn_fold": 1, "p5": 1, "p5_split": 0, "splitk_inl": 1, "p4_plain": 1, "splitk": 1,
+                                 "attn_split": 1, "p4_sub": 1, "gn_wide": 1, "small_conv": 1, "conv_variant": 2}.get(k, 0))
             print(f"round {r} {v}: {ms:.4f} ms/step", flush=True)
     for v in variants:
         print(f"{v}: best {min(res[v]):.4f} ms/step  ({args.n * 1000 / min(res[v]) / 1000 * 1000 / 1000:.2f} cand/s at T=1000)")
