@@ -28,6 +28,7 @@ template <typename T> hipError_t launch_conv(const ConvArgs&, hipStream_t);
 template <typename T> hipError_t launch_groupnorm(const GNArgs&, int, hipStream_t);
 template <typename T> hipError_t launch_attn(const AttnArgs&, int, hipStream_t);
 bool attn_flash_ok(int S, int C);
+bool attn_cs_ok(int S, int C);
 bool attn_block_ok(int S, int C);
 hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
 int g_attn_fuse = 1;  // fused AttnBlock kernel where it applies (itsd_set_option "attn_fuse", read at create)
@@ -571,7 +572,7 @@ struct Builder {
       const int S = H * W;
       int vt = -1;
       // (S <= 256: whole-row MFMA kernel; longer sequences: flash kernel, C <= 256)
-      if (u->bf16 && S % 16 == 0 && out_ch % 64 == 0 && (S <= 256 || attn_flash_ok(S, out_ch))) {
+      if (u->bf16 && S % 16 == 0 && out_ch % 64 == 0 && (S <= 256 || attn_flash_ok(S, out_ch) || attn_cs_ok(S, out_ch))) {
         vt = act(out_ch, S, 1);
         u->ops.back().vt = vt;
         u->ops.back().vt_from = 2 * out_ch;
@@ -1180,6 +1181,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_io_mfma = value ? 1 : 0;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "small_wide")) {  // conv_small for under-filled statistics-free convs of larger images
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_wide in [0,1]");
+    itsd::g_small_wide = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "small_conv")) {
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "small_conv in [0,2]");
     itsd::g_small_conv = value;
@@ -1250,6 +1256,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_sub = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "subpix_split")) {  // under-filled sub-pixel conv_pipe launches split K in-launch
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "subpix_split in [0,1]");
+    itsd::g_subpix_split = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p4_plain")) {  // plain 3x3 stride-1 convs on conv3x3_gn_p4_kernel (halo copies the input)
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_plain in [0,1]");
     itsd::g_p4_plain = value;
@@ -1281,6 +1292,16 @@ int itsd_set_option(const char* key, int value) {
   }
   if (!std::strcmp(key, "down_merge")) {  // CFG DownSample c1 + c2 as one 5x5 conv (UNets created afterwards)
     itsd::g_down_merge = value ? 1 : 0;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_wide_nq")) {  // channel-split attention: query groups a block (0 auto, 1, 2)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_wide_nq in [0,2]");
+    itsd::g_attn_wide_nq = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_wide")) {  // channel-split attention (attn_cs_kernel): 0 off, 1 auto (C >= 384, S >= 256), 2 wherever it applies
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_wide in [0,2]");
+    itsd::g_attn_wide = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards
@@ -1540,7 +1561,7 @@ int itsd_attention(const void* qkv, const void* vt, void* out, int n, int S, int
   if (precision == ITSD_PREC_BF16) {
     if (C % 8) return fail(ITSD_ERR_INVALID, "C must be a multiple of 8");
     if (vt) {
-      if (S % 16 || C % 64 || (S > 256 && !attn_flash_ok(S, C)))
+      if (S % 16 || C % 64 || (S > 256 && !attn_flash_ok(S, C) && !attn_cs_ok(S, C)))
         return fail(ITSD_ERR_INVALID, "MFMA attention needs S % 16 == 0, C % 64 == 0 (S > 256: C in {64,128,256})");
       a.vt = vt;
     }

@@ -41,6 +41,8 @@ int g_fuse_gn = 1;
 int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
+int g_small_wide = 1;    // ... also for statistics-free convs of larger images (64-pixel tiles inside one image)
+                         // whose 128x128 conv_pipe grid under-fills the chip (small batches) ("small_wide")
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
 int g_gn_reg = 4;        // the 256-pixel fused GroupNorm conv: 4 = conv3x3_gn_p4_kernel (the only shipped
@@ -51,6 +53,7 @@ int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
+int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
@@ -469,7 +472,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
   const int HWo = a.Hout * a.Wout;
   // sub-pixel phase: (subpix 1, nearest-x2 upsample convs) 2x2 taps at input offsets (dy + py - 1,
   // dx + px - 1); (subpix 2, CFG ConvTranspose2d(5, 2, 2, 1)) 3x3 taps at (dy - 1, dx - 1) for every phase
-  const int phase = a.subpix ? bt.z : -1;
+  // (sub-pixel launches: z = phase + 4 x K slice)
+  const int phase = a.subpix ? (bt.z & 3) : -1;
   const int padY = a.subpix == 1 ? 1 - (phase >> 1) : a.pad, padX = a.subpix == 1 ? 1 - (phase & 1) : a.pad;
   const T* wbase = (const T*)a.wt + (a.subpix ? (size_t)phase * a.Cout * a.K : 0);
   const int Hv = a.upsample ? 2 * a.Hin : (a.zins ? 2 * a.Hin - 1 : a.Hin);
@@ -552,8 +556,8 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
 
   f32x16 acc[2][2];
   zero_acc(acc);
-  // split-K: slice z of gridDim.z covers K-stages [k0, k1) (sub-pixel launches use z as phase)
-  const int S = a.subpix ? 1 : gridDim.z, z = a.subpix ? 0 : bt.z;
+  // split-K: slice z covers K-stages [k0, k1) (sub-pixel launches: gridDim.z = 4 phases x S slices)
+  const int S = a.subpix ? (int)(gridDim.z >> 2) : (int)gridDim.z, z = a.subpix ? (bt.z >> 2) : bt.z;
   const int k0 = (int)((long long)nK * z / S), k1 = (int)((long long)nK * (z + 1) / S);
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -580,7 +584,7 @@ __global__ __launch_bounds__(256, (NS <= 2 ? 2 : 1)) void conv_pipe(ConvArgs a) 
     // drained by every wave; the slice drawing ticket S-1 sums slices 0..S-1 in order
     const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
         a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
-    const int tile = bt.y * gridDim.x + bt.x;
+    const int tile = ((a.subpix ? phase : 0) * gridDim.y + bt.y) * gridDim.x + bt.x;  // (host: tickets for all)
     const uint32_t base = (uint32_t)((size_t)tile * S * 65536) + threadIdx.x * 16;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -812,8 +816,11 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
 // Host-side eligibility of conv_small (bf16, whole 128-B K-chunks, plain stride/pad addressing).
 bool conv_small_ok(const ConvArgs& a) {
   const int HWo = a.Hout * a.Wout, Cin = a.C1 + a.C2;
+  // (tiles of whole images -- their statistics slots and additive rows -- or, without a consumer
+  // GroupNorm, 64-pixel tiles inside one image)
   return a.zero && !a.subpix && !a.upsample && !a.zins && !a.gn_coef && Cin % 64 == 0 && a.C1 % 64 == 0 &&
-         a.K == a.ksize * a.ksize * Cin && a.ksize <= 5 && HWo <= SM_B && SM_B % HWo == 0 &&
+         a.K == a.ksize * a.ksize * Cin && a.ksize <= 5 &&
+         ((HWo <= SM_B && SM_B % HWo == 0) || (g_small_wide && !a.stats && HWo % SM_B == 0)) &&
          (!a.vt_out || HWo % 8 == 0);
 }
 
@@ -3118,7 +3125,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // (in-launch combine), up to ~2 blocks per CU with >= 2 K-chunks a slice.
     dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
     int S = 1;
-    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk && a.Hout * a.Wout <= 16 &&
+    // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
+    const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < 256;
+    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk && (a.Hout * a.Wout <= 16 || wide) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
       const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
       S = std::min(std::min((512 + blocks - 1) / blocks, nK / 2), 16);  // <= 2 combine batches
@@ -3126,7 +3135,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       if (S < 1) S = 1;
     }
     if (g_small_conv && conv_small_ok(a) &&
-        (g_small_conv == 2 || S > 1 ||
+        (g_small_conv == 2 || S > 1 || wide ||
          (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
       gs.z = S;
       if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);
@@ -3158,6 +3167,16 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       }
     }
     grid.z = 4;
+    // under-filled grids (the 4x4 -> 8x8 upsample at small batches, the CFG ConvTranspose2d from the 2x2
+    // grid: 32-64 blocks): split K with the in-launch combine, the tiles' tickets per (phase, tile)
+    if (a.splitk_ws && a.tickets && g_splitk && g_splitk_inl && g_subpix_split) {
+      const int blocks = (int)(grid.x * grid.y) * 4;
+      const int nK = a.ksize * a.ksize * (Cin / BK);
+      int S = 1;
+      if (blocks < 256 && blocks <= kTicketCap) S = std::min((512 + blocks - 1) / blocks, nK / 8);
+      while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
+      if (S > 1) grid.z = 4 * S;
+    }
     ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }

@@ -1074,6 +1074,8 @@ extern "C" int itsd_debug_stamps_attn(unsigned long long* host) {
 }
 #endif
 
+int g_attn_wide_nq = 1;  // its query groups a block: 0 auto, 1 / 2 forced (2 measured equal at C3, slower at C4) (itsd_set_option "attn_wide_nq")
+int g_attn_wide = 1;   // channel-split attention: 0 off, 1 auto (C >= 384, S >= 256), 2 wherever attn_cs_ok (itsd_set_option "attn_wide")
 int g_attn_split = 1;  // attn_block_split_kernel for small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 // G blocks per image for attn_block_split_kernel at batch n (0: one block per image, attn_block_kernel):
 // the largest of 6 / 4 / 2 that keeps the grid co-resident (n * G <= CUs, one block per CU)
@@ -1232,6 +1234,131 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
 #undef ITSD_FLASH_LSTORE
 }
 
+// Channel-split attention for wide channels (C = 256 .. 512, S % 32 == 0: Arch A's 16x16 level at
+// 64 px (S = 256, C = 384), the CFG model's 16x16 level (S = 256, C = 512)), where one wave cannot hold
+// q and O for all C channels. A block takes 32 queries; wave w owns channels [w C/4, (w+1) C/4) for
+// BOTH products, so every K / V byte is read once per block with no LDS staging:
+//  - per 32-key tile each wave computes a partial s^T = K_w q_w^T over its channels (C/64 MFMAs,
+//    K fragments prefetched a tile ahead), writes it to LDS, and after one barrier every wave sums
+//    the 4 partials in wave order (identical scores in all waves: deterministic), runs the online
+//    softmax and O_w^T += V_w^T P^T on its own C/128 channel blocks (V^T fragments prefetched a tile
+//    ahead, the flash kernel's key permutation);
+//  - the partial-score buffer is double-buffered by tile parity: one barrier a tile.
+template <int C, int NQ>
+__global__ __launch_bounds__(256 * NQ) void attn_cs_kernel(AttnArgs a) {
+  constexpr int CQ = C / 4, QS = CQ / 16, CB = CQ / 32, C3 = 3 * C;
+  static_assert(CQ % 32 == 0, "whole 32-channel blocks a wave");
+  // [tile parity][query group][wave of the group][r / 4][lane][r % 4]
+  __shared__ __attribute__((aligned(16))) float Sp[2][NQ][4][4][64][4];
+  const int S = a.S, QT = S / (32 * NQ);
+  const int nb = gridDim.x, bx = blockIdx.x;
+  const int L = (nb & 7) ? bx : (bx & 7) * (nb >> 3) + (bx >> 3);  // XCD-major: an image's tiles on one XCD
+  const int img = L / QT, qt = L - img * QT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3, qg = tid >> 8, rl = lane & 31, hh = lane >> 5;
+  const int q = (qt * NQ + qg) * 32 + rl, ch0 = wid * CQ;
+  const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
+  const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
+  bf16x8 qf[QS], kf[QS];
+  {
+    const bf16_t* qp = base + (size_t)q * C3 + ch0 + 8 * hh;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) qf[i] = *(const bf16x8*)(qp + 16 * i);
+    const bf16_t* kp = base + (size_t)rl * C3 + C + ch0 + 8 * hh;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) kf[i] = *(const bf16x8*)(kp + 16 * i);
+  }
+  // V^T fragments of tile kt: lane (channel rl of block cb, hi) keys {16j+4hi+0..3, 16j+8+4hi+0..3}
+  u32x4 vf[CB][2];
+  auto load_v = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      const bf16_t* vp = vt + (size_t)(ch0 + cb * 32 + rl) * S + kt + 4 * hh;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint2 lo = *(const uint2*)(vp + 16 * j), hi = *(const uint2*)(vp + 16 * j + 8);
+        vf[cb][j] = u32x4{lo.x, lo.y, hi.x, hi.y};
+      }
+    }
+  };
+  load_v(0);
+  f32x16 o[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[cb][r] = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;  // softmax via exp2
+  float m = -INFINITY, l = 0.f;
+  const int nt = S / 32;
+  for (int t = 0; t < nt; ++t) {
+    const int kt = t * 32, par = t & 1;
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], s, 0, 0, 0);
+    if (t + 1 < nt) {  // next tile's K fragments (their latency behind the exchange, softmax and PV)
+      const bf16_t* kp = base + (size_t)(kt + 32 + rl) * C3 + C + ch0 + 8 * hh;
+#pragma unroll
+      for (int i = 0; i < QS; ++i) kf[i] = *(const bf16x8*)(kp + 16 * i);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(f32x4*)&Sp[par][qg][wid][g][lane][0] = f32x4{s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]};
+    __syncthreads();  // (Sp[par] of tile t - 2 was read before this barrier's predecessor)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v = *(const f32x4*)&Sp[par][qg][0][g][lane][0];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += *(const f32x4*)&Sp[par][qg][w][g][lane][0];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[4 * g + e] = v[e] * sl2;
+    }
+    // s[r] = scaled score(query rl, key kt + (r&3) + 8(r>>2) + 4hh)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = exp2f(s[r] - mn);
+      rs += s[r];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf16x8 bp;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bp[i] = (short)f2bf(s[8 * j + i]);
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+        o[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vf[cb][j]), bp, o[cb], 0, 0, 0);
+    }
+    if (t + 1 < nt) load_v(kt + 32);
+  }
+  const float inv = 1.0f / l;
+  bf16_t* out = (bf16_t*)a.out + ((size_t)img * S + q) * C + ch0;
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = cb * 32 + 8 * g + 4 * hh;
+      uint2 w2;
+      w2.x = (uint32_t)f2bf(o[cb][4 * g] * inv) | ((uint32_t)f2bf(o[cb][4 * g + 1] * inv) << 16);
+      w2.y = (uint32_t)f2bf(o[cb][4 * g + 2] * inv) | ((uint32_t)f2bf(o[cb][4 * g + 3] * inv) << 16);
+      *(uint2*)(out + c) = w2;
+    }
+}
+bool attn_cs_ok(int S, int C) { return S % 64 == 0 && (C == 256 || C == 384 || C == 512); }
+
 bool attn_flash_ok(int S, int C) { return S % 32 == 0 && (C == 64 || C == 128 || C == 256); }
 
 size_t attn_mfma_smem(int S) {
@@ -1242,6 +1369,22 @@ size_t attn_mfma_smem(int S) {
 template <typename T>
 hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
+    // channel-split attention: auto (g_attn_wide = 1) for C >= 384 at S >= 256; 2 = wherever it applies
+    if (a.vt && g_attn_wide && attn_cs_ok(a.S, a.C) && (g_attn_wide == 2 || (a.C >= 384 && a.S >= 256))) {
+      // 64 queries (two groups of 4 waves) a block; 32 when the query tiles of 64 leave CUs idle
+      if (g_attn_wide_nq == 2 || (g_attn_wide_nq == 0 && (long long)(a.S / 64) * n >= g_num_cus)) {
+        const dim3 grid((unsigned)((a.S / 64) * n));
+        if (a.C == 512) ITSD_LAUNCH((attn_cs_kernel<512, 2>), grid, dim3(512), 0, s, a);
+        else if (a.C == 384) ITSD_LAUNCH((attn_cs_kernel<384, 2>), grid, dim3(512), 0, s, a);
+        else ITSD_LAUNCH((attn_cs_kernel<256, 2>), grid, dim3(512), 0, s, a);
+      } else {
+        const dim3 grid((unsigned)((a.S / 32) * n));
+        if (a.C == 512) ITSD_LAUNCH((attn_cs_kernel<512, 1>), grid, dim3(256), 0, s, a);
+        else if (a.C == 384) ITSD_LAUNCH((attn_cs_kernel<384, 1>), grid, dim3(256), 0, s, a);
+        else ITSD_LAUNCH((attn_cs_kernel<256, 1>), grid, dim3(256), 0, s, a);
+      }
+      return hipGetLastError();
+    }
     if (a.vt && a.S > 256) {
       if (!attn_flash_ok(a.S, a.C)) return hipErrorInvalidValue;
       const dim3 grid((unsigned)(((a.S + 127) / 128) * n));

@@ -278,28 +278,60 @@ def _attn_ref(qkv):
     return torch.bmm(torch.softmax(w, dim=-1), v)
 
 
-@pytest.mark.parametrize("n,S,C,dtype,with_vt", [
-    (2, 1024, 128, torch.bfloat16, True),   # C3 level 0: flash kernel
-    (1, 4096, 256, torch.bfloat16, True),   # Arch A at 256 px, level 2: flash kernel
-    (3, 320, 64, torch.bfloat16, True),     # flash kernel, ragged last key tile
-    (2, 64, 384, torch.bfloat16, True),     # Arch A level 2: whole-row MFMA kernel
-    (2, 16, 1024, torch.bfloat16, True),    # C3 level 3
-    (2, 4, 512, torch.bfloat16, False),     # C3 level 4: VALU kernel
-    (2, 1024, 128, torch.float32, False),   # parity mode
-    (3, 1, 256, torch.float32, False),      # C3 level 5 (S = 1: softmax of one key)
+@pytest.mark.parametrize("n,S,C,dtype,with_vt,wide", [
+    (2, 256, 384, torch.bfloat16, True, 1),   # Arch A at 64 px, level 2 (C4): channel-split kernel
+    (3, 256, 512, torch.bfloat16, True, 1),   # C3 level 1: channel-split kernel
+    (2, 1024, 256, torch.bfloat16, True, 2),  # channel-split forced where the flash kernel runs
+    (2, 64, 256, torch.bfloat16, True, 2),    # channel-split forced at S = 64
+    (2, 1024, 128, torch.bfloat16, True, 1),  # C3 level 0: flash kernel
+    (1, 4096, 256, torch.bfloat16, True, 1),  # Arch A at 256 px, level 2: flash kernel
+    (3, 320, 64, torch.bfloat16, True, 1),    # flash kernel, ragged last query tile
+    (2, 64, 384, torch.bfloat16, True, 1),    # Arch A level 2: whole-row MFMA kernel
+    (2, 16, 1024, torch.bfloat16, True, 1),   # C3 level 3
+    (2, 4, 512, torch.bfloat16, False, 1),    # C3 level 4: VALU kernel
+    (2, 1024, 128, torch.float32, False, 1),  # parity mode
+    (3, 1, 256, torch.float32, False, 1),     # C3 level 5 (S = 1: softmax of one key)
 ])
-def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt):
+def test_attention_kernels_vs_torch(n, S, C, dtype, with_vt, wide):
     gen = torch.Generator().manual_seed(S + C)
     qkv = (torch.randn(n, S, 3 * C, generator=gen) * 1.5).to(dtype)
     ref = _attn_ref(qkv)
     d = qkv.cuda()
     vt = d[:, :, 2 * C:].transpose(1, 2).contiguous() if with_vt else None
-    out = rt.attention(d, vt).float().cpu()
+    rt.set_option("attn_wide", wide)
+    try:
+        out = rt.attention(d, vt).float().cpu()
+        assert torch.equal(out, rt.attention(d, vt).float().cpu())  # deterministic
+    finally:
+        rt.set_option("attn_wide", 1)
     if dtype == torch.float32:
         np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=5e-5, rtol=0)  # fp32, S-term sums
     else:  # P and the output are rounded to bf16
         assert _rel_l2(out, ref) < 1e-2
         assert (out - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("S,C", [(256, 384), (256, 512), (1024, 256)])
+def test_channel_split_attention_query_groups_bit_identical(S, C):
+    """attn_cs_kernel with 2 query groups a block (512 threads) computes every query exactly as with one
+    (the same wave-level products and partial-score order): bit-identical outputs, and within the bf16
+    bound of the fp32 reference."""
+    n = 3
+    gen = torch.Generator().manual_seed(7 * S + C)
+    qkv = (torch.randn(n, S, 3 * C, generator=gen) * 1.5).to(torch.bfloat16)
+    d = qkv.cuda()
+    vt = d[:, :, 2 * C:].transpose(1, 2).contiguous()
+    outs = []
+    rt.set_option("attn_wide", 2)
+    try:
+        for nq in (1, 2):
+            rt.set_option("attn_wide_nq", nq)
+            outs.append(rt.attention(d, vt).float().cpu())
+    finally:
+        rt.set_option("attn_wide", 1)
+        rt.set_option("attn_wide_nq", 1)
+    assert torch.equal(outs[0], outs[1])
+    assert _rel_l2(outs[1], _attn_ref(qkv)) < 1e-2
 
 
 _TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 4, "p4_sub": 1}
@@ -471,6 +503,69 @@ def test_p4_subpixel_convtranspose_vs_conv_pipe_cfg():
         ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
     d, e = _rel_l2(sub, pipe), _rel_l2(sub[idx], ref)
     print(f"CFG 2N=64: p4 sub-pixel ConvTranspose vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("arch,n", [(ARCH_C, 64), (ARCH_A, 8)])
+def test_subpixel_split_k_vs_unsplit(arch, n):
+    """Under-filled sub-pixel conv_pipe launches (the CFG ConvTranspose2d from the 2x2 grid at 2N = 64:
+    32 blocks; Arch A's 4x4 -> 8x8 upsample at n = 8: 16 blocks) split K over 4 phases x S slices with
+    the in-launch combine (tickets per (phase, tile), slices summed in order): deterministic, within
+    1e-2 relative L2 of the unsplit launch (subpix_split = 0), and within the bf16 bound of the oracle."""
+    net = _net(arch, "bf16")
+    gen = torch.Generator().manual_seed(650 + n)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, arch.T, (n,), generator=gen)
+    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n - n // 2, dtype=torch.long)]) if arch.cfg else None
+    args = [xc.cuda(), tc.cuda()] + ([lab.cuda()] if arch.cfg else [])
+
+    def run(split):
+        rt.set_option("subpix_split", split)
+        try:
+            return net(*args).float().cpu()
+        finally:
+            rt.set_option("subpix_split", 1)
+
+    sp = run(1)
+    assert torch.equal(sp, run(1))
+    un = run(0)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(arch, synthetic_state_dict(arch, 0))(xc[idx], tc[idx], *([lab[idx]] if arch.cfg else []))
+    d, e = _rel_l2(sp, un), _rel_l2(sp[idx], ref)
+    print(f"{arch.kind} n={n}: sub-pixel split-K vs unsplit rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16  # (measured 5.7e-3 / 7.8e-3: one conv's sum order, through the net)
+
+
+@pytest.mark.parametrize("n", [16, 32])
+def test_small_wide_stats_free_convs_vs_conv_pipe(n):
+    """Small batches: the statistics-free convs of 8x8 .. 32x32 images (ResBlock shortcuts, the q|k|v
+    convs) whose 128x128 conv_pipe grid under-fills the chip run on conv_small's 64x64 tiles (inside
+    one image, split K): deterministic, within 1e-2 relative L2 of conv_pipe (small_wide = 0) and
+    within the bf16 bound of the oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(660 + n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    assert any(o["kind"] == "conv" and o["H"] >= 8 and o["ks"] == 1 and "conv_small" in o["kernel"] for o in ops)
+
+    def run(v):
+        rt.set_option("small_wide", v)
+        try:
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("small_wide", 1)
+
+    w = run(1)
+    assert torch.equal(w, run(1))
+    p = run(0)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    d, e = _rel_l2(w, p), _rel_l2(w[idx], ref)
+    print(f"n={n}: conv_small (wide) vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
     assert d < 1e-2 and e < REL_L2_BF16
 
 
