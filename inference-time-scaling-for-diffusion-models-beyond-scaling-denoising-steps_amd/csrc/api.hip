@@ -1181,6 +1181,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_io_mfma = value ? 1 : 0;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "conv1x1")) {  // streaming 1x1 conv kernel for statistics-free 1x1 convs of large pixel counts
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "conv1x1 in [0,2]");
+    itsd::g_conv1x1 = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "small_wide")) {  // conv_small for under-filled statistics-free convs of larger images
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_wide in [0,1]");
     itsd::g_small_wide = value;

@@ -41,6 +41,8 @@ int g_fuse_gn = 1;
 int g_conv_dbg = 0;
 int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
+int g_conv1x1 = 1;       // streaming 1x1 kernel for statistics-free 1x1 convs of large pixel counts: 0 off,
+                         // 1 on (4-stage ring), 2 on (7-stage ring) ("conv1x1")
 int g_small_wide = 1;    // ... also for statistics-free convs of larger images (64-pixel tiles inside one image)
                          // whose 128x128 conv_pipe grid under-fills the chip (small batches) ("small_wide")
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
@@ -811,6 +813,132 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
   }
   __syncthreads();
   epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true>(a, smem, tileP, tileC, -1);
+}
+
+// ---------------------------------------------------------------------------- streaming 1x1
+// Statistics-free 1x1 convs of large pixel counts (the ResBlock shortcuts at the 32x32 / 16x16 levels
+// at N = 256: K = 256..640, Cout = 128 / 256) are HBM streams (~4 bytes of input per MFMA flop-pair
+// ... 128 flops a byte): conv_pipe reloads the weights per 128x128 tile and drains its pipeline per
+// tile (~45 % of HBM bandwidth). Here a persistent block keeps one 128-cout tile's weights in
+// VGPRs for the whole launch (wave w: couts 32w..32w+31, all CIN as CIN/16 A fragments straight from
+// the [Cout][K] rows) and streams 128-pixel tiles through a 4-stage global_load_lds ring of 64-channel
+// chunks that runs across tile boundaries (the next tile's loads fly during the epilogue); the
+// epilogue rounds acc + bias into an LDS tile and stores it as coalesced 16-B rows. Blocks are dealt
+// XCD-major: the blocks of the cout tiles of one pixel tile share an XCD (its L2 serves the second read).
+// NS ring stages (64-channel chunks of 128 pixels, 16 KB each; NS = 7: 96 KB in flight a CU)
+constexpr int S1_OROW = 272;                // out-tile row bytes (128 couts bf16 + 16 B pad: 16-B aligned)
+// s_waitcnt vmcnt(n) for a run-time n in {0, 4, .., N} (wave-uniform)
+template <int N>
+__device__ __forceinline__ void s1_wait_from(int n) {
+  if constexpr (N < 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else s1_wait_from<N - 4>(n);
+  }
+}
+
+template <int CIN, int S1_NS>
+__global__ __launch_bounds__(256, 1) void conv1x1_stream_kernel(ConvArgs a) {
+  typedef bf16_t T;
+  constexpr int NK = CIN / 16, NCH = CIN / 64;
+  __shared__ __attribute__((aligned(16))) char smem[S1_NS * TILEB + 128 * S1_OROW];
+  char* const otile = smem + S1_NS * TILEB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
+  const int G = gridDim.x, b = blockIdx.x;  // host: G % (8 nTC) == 0
+  const int xcd = b & 7, j = b >> 3, tc = j % nTC, slot = (j / nTC) * 8 + xcd, GS = G / nTC;
+  const int ntile = slot < nTP ? (nTP - 1 - slot) / GS + 1 : 0;
+  if (ntile == 0) return;
+  const int co0 = tc * CONV_BM + 32 * wid;
+  // weights: A fragment of k-step s = W[co0 + rl][16 s + 8 hh .. +7]
+  bf16x8 wa[NK];
+#pragma unroll
+  for (int s = 0; s < NK; ++s) wa[s] = *(const bf16x8*)((const T*)a.wt + (size_t)(co0 + rl) * a.K + 16 * s + 8 * hh);
+  float bias[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[g][e] = a.bias[co0 + 8 * g + 4 * hh + e];
+  // DMA rows: instruction q of wave w fills rows 8 (4w + q) .. +7 of a stage (lane -> row + lane / 8,
+  // slot lane % 8 <- logical 16-B chunk (lane % 8) ^ ((row >> 1) & 7): swz's image)
+  int roff[4], coff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 8 * (4 * wid + q) + (lane >> 3);
+    roff[q] = r;
+    coff[q] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+  }
+  const int nst = ntile * NCH;  // the block's chunk sequence: tile i = slot + i GS, chunk cc
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const int i = st / NCH, cc = st - i * NCH, tp = slot + i * GS;
+    const int ci0 = cc * 64;
+    const bool s1 = ci0 < a.C1;
+    const T* src = s1 ? (const T*)a.src1 : (const T*)a.src2;
+    const int Cs = s1 ? a.C1 : a.C2, cs0 = s1 ? ci0 : ci0 - a.C1;
+    char* dst = smem + (st % S1_NS) * TILEB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const T* g = src + (size_t)(tp * CONV_BN + roff[q]) * Cs + cs0 + coff[q];
+      __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(dst + (4 * wid + q) * 1024), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < S1_NS - 1; ++st)
+    if (st < nst) issue(st);
+  f32x16 acc[4];
+  for (int i = 0; i < ntile; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[jj][r] = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) {  // (unrolled: the weight fragments are indexed at compile time)
+      const int st = i * NCH + cc;
+      // stage st landed: the younger stages (4 DMA each) and, after a tile's end, its 8 output stores
+      // (younger than that step's DMA) may still fly
+      const int ahead = min(S1_NS - 2, nst - 1 - st);
+      s1_wait_from<4 * (S1_NS - 2) + 8>(4 * ahead + (cc == 0 && i > 0 ? 8 : 0));
+      __builtin_amdgcn_s_barrier();
+      if (st + S1_NS - 1 < nst) issue(st + S1_NS - 1);  // (its slot was read in step st - 1)
+      const char* B = smem + (st % S1_NS) * TILEB;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 bf[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) bf[jj] = *(const bf16x8*)(B + swz(32 * jj + rl, 2 * ks + hh));
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cc * 4 + ks], bf[jj], acc[jj], 0, 0, 0);
+      }
+    }
+    // acc (+ bias) -> bf16 out tile [pixel][128 couts]: lane (pixel 32 jj + rl), couts 8 g + 4 hh .. +3
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 w2;
+        w2.x = (uint32_t)f2bf(acc[jj][4 * g] + bias[g][0]) | ((uint32_t)f2bf(acc[jj][4 * g + 1] + bias[g][1]) << 16);
+        w2.y = (uint32_t)f2bf(acc[jj][4 * g + 2] + bias[g][2]) | ((uint32_t)f2bf(acc[jj][4 * g + 3] + bias[g][3]) << 16);
+        *(uint2*)(otile + (32 * jj + rl) * S1_OROW + (32 * wid + 8 * g + 4 * hh) * 2) = w2;
+      }
+    __syncthreads();
+    const int tp = slot + i * GS;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // 128 pixels x 16 chunks of 16 B
+      const int u = tid + 256 * k, pr = u >> 4, ch = u & 15;
+      const u32x4 v = *(const u32x4*)(otile + pr * S1_OROW + ch * 16);
+      *(u32x4*)((T*)a.out + (size_t)(tp * CONV_BN + pr) * a.Cout + tc * CONV_BM + ch * 8) = v;
+    }
+    // (the next tile's epilogue writes the out tile only after >= 1 more ring barrier)
+  }
+}
+bool conv1x1_stream_ok(const ConvArgs& a) {
+  const int Cin = a.C1 + a.C2;
+  return a.zero && a.ksize == 1 && a.stride == 1 && a.pad == 0 && !a.subpix && !a.upsample && !a.zins && !a.gn_coef &&
+         !a.stats && !a.temb && !a.cemb && !a.resid && !a.vt_out && a.C1 % 64 == 0 && a.C2 % 64 == 0 &&
+         (Cin == 256 || Cin == 384 || Cin == 512 || Cin == 640) && a.K == Cin && a.Cout % CONV_BM == 0 &&
+         a.M % CONV_BN == 0;
 }
 
 // Host-side eligibility of conv_small (bf16, whole 128-B K-chunks, plain stride/pad addressing).
@@ -2878,14 +3006,24 @@ __global__ __launch_bounds__(256, 2) void head_mfma_kernel(HeadArgs h) {
   const int rows = HW >= 128 ? 128 / W : h.H;         // output rows per image in the tile
   const int y0 = r0 / W, TR = rows + 2, TW = W + 2;
   float* tin = (float*)smem + 128 * 132;              // [nimg][3][TR][TW] behind the epilogue's E tile
-  for (int i = tid; i < nimg * 3 * TR * TW; i += 256) {
-    const int im = i / (3 * TR * TW), r = i - im * 3 * TR * TW;
-    const int ci = r / (TR * TW), q = r - ci * TR * TW, ty = q / TW, tx = q - ty * TW;
-    const int iy = y0 - 1 + ty, ix = tx - 1, img = img0 + im;
-    float v = 0.0f;
-    if (img < h.n && iy >= 0 && iy < h.H && ix >= 0 && ix < W)
-      v = h.x[((size_t)(img % h.x_img_mod) * 3 + ci) * HW + iy * W + ix];
-    tin[i] = v;
+  // 4 window elements a thread per batch, all loads (from clamped addresses) issued before any use:
+  // one memory round trip for the 32 x 32 window (612 elements)
+  const int tot = nimg * 3 * TR * TW;
+  for (int i0 = tid; i0 < tot; i0 += 4 * 256) {
+    float v[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 256 * u;
+      const int im = i / (3 * TR * TW), r = i - im * 3 * TR * TW;
+      const int ci = r / (TR * TW), q = r - ci * TR * TW, ty = q / TW, tx = q - ty * TW;
+      const int iy = y0 - 1 + ty, ix = tx - 1, img = img0 + im;
+      ok[u] = i < tot && img < h.n && iy >= 0 && iy < h.H && ix >= 0 && ix < W;
+      v[u] = h.x[ok[u] ? ((size_t)(img % h.x_img_mod) * 3 + ci) * HW + iy * W + ix : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + 256 * u < tot) tin[i0 + 256 * u] = ok[u] ? v[u] : 0.0f;
   }
   // A fragments (weights) straight from the prepacked [Cout][32] bf16 matrix
   bf16x8 af[4][2];
@@ -3117,6 +3255,26 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     }
   }
   if constexpr (sizeof(T) == 2) {
+    // streaming 1x1 convs: >= 4 pixel tiles per persistent block (large pixel counts, N = 256)
+    if (g_conv1x1 && conv1x1_stream_ok(a)) {
+      const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
+      int G = (g_num_cus / (8 * nTC)) * 8 * nTC;  // whole XCD rounds of every cout tile
+      if (G > 0 && (long long)nTP * nTC >= 4LL * G) {
+        const int Cin = a.C1 + a.C2;
+#define ITSD_S1(NS)                                                                          \
+  if (Cin == 256) ITSD_LAUNCH((conv1x1_stream_kernel<256, NS>), dim3(G), dim3(256), 0, s, a);      \
+  else if (Cin == 384) ITSD_LAUNCH((conv1x1_stream_kernel<384, NS>), dim3(G), dim3(256), 0, s, a); \
+  else if (Cin == 512) ITSD_LAUNCH((conv1x1_stream_kernel<512, NS>), dim3(G), dim3(256), 0, s, a); \
+  else ITSD_LAUNCH((conv1x1_stream_kernel<640, NS>), dim3(G), dim3(256), 0, s, a);
+        if (g_conv1x1 == 2) {
+          ITSD_S1(7)
+        } else {
+          ITSD_S1(4)
+        }
+#undef ITSD_S1
+        return hipGetLastError();
+      }
+    }
     // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
     // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
     // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured

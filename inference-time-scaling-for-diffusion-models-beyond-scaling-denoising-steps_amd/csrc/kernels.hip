@@ -1776,18 +1776,30 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   }
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int cpp = C / 8, npx = (rpb + 2) * (W + 2), total = npx * cpp;
+  // the sampler step's operands of this thread's output items (it = tid, tid + 256), loaded now: their
+  // latency hides behind the halo staging and the MFMAs
+  constexpr int TIT = (TM_PX * 3 + 255) / 256;
+  float xpre[TIT];
+  int tpre = 0;
+  if (a.step_mode) {
+    tpre = *a.tsel;
+#pragma unroll
+    for (int k = 0; k < TIT; ++k) {
+      const int it = tid + 256 * k, opx = it < TM_PX * 3 ? it / 3 : 0, oc = it < TM_PX * 3 ? it - opx * 3 : 0;
+      const int rem = (y0 + opx / W) * W + (opx - (opx / W) * W);
+      xpre[k] = a.x[((size_t)img * 3 + oc) * HW + rem];
+    }
+  }
+  constexpr int TB = 16;  // halo items a thread per batch (C = 128, 32 x 32: the whole halo in one batch)
   for (int pass = 0; pass < (a.cfg ? 2 : 1); ++pass) {
     const int im = img + pass * a.n;
     __syncthreads();
     const bf16_t* gb = (const bf16_t*)a.g + (size_t)im * HW * C;
-    // the image's GroupNorm coefficients, once in LDS
-    for (int i = tid; i < cpp * 16; i += 256) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
-    __syncthreads();
-    for (int i0 = 0; i0 < total; i0 += 8 * 256) {
-      u32x4 v[8];
-      int dst[8];
+    for (int i0 = 0; i0 < total; i0 += TB * 256) {
+      u32x4 v[TB];
+      int dst[TB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // all loads of the batch first
+      for (int u = 0; u < TB; ++u) {  // all loads of the batch first
         const int i = i0 + u * 256 + tid;
         const int hp = i / cpp, ch = i - hp * cpp;
         const int hy = hp / (W + 2), hx = hp - hy * (W + 2);
@@ -1797,8 +1809,12 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
         v[u] = ok ? *(const u32x4*)(gb + ((size_t)gy * W + gx) * C + ch * 8) : u32x4{0u, 0u, 0u, 0u};
         if (!ok) dst[u] = i < total ? -2 - dst[u] : -1;  // padding: store zeros at -2 - dst
       }
+      if (i0 == 0) {  // the image's GroupNorm coefficients, once in LDS (their loads behind the batch's)
+        for (int i = tid; i < cpp * 16; i += 256) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
+        __syncthreads();
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < TB; ++u) {
         if (dst[u] == -1) continue;
         u32x4 y = {0u, 0u, 0u, 0u};
         int d = dst[u];
@@ -1845,7 +1861,10 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     }
   }
   __syncthreads();
-  for (int it = tid; it < TM_PX * 3; it += 256) {
+#pragma unroll
+  for (int k = 0; k < TIT; ++k) {
+    const int it = tid + 256 * k;
+    if (it >= TM_PX * 3) break;
     const int opx = it / 3, oc = it - opx * 3;
     float e = red[opx * 3 + oc] + a.b[oc];
     if (a.cfg) {
@@ -1861,8 +1880,8 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     }
     {
 #pragma clang fp contract(off)
-      const int t = *a.tsel;
-      const float xv = a.x[o];
+      const int t = tpre;
+      const float xv = xpre[k];
       const float mean = a.coeff1[t] * xv - a.coeff2[t] * e;
       float xn = mean;
       if (t > 0) {

@@ -537,6 +537,35 @@ def test_subpixel_split_k_vs_unsplit(arch, n):
     assert d < 1e-2 and e < REL_L2_BF16  # (measured 5.7e-3 / 7.8e-3: one conv's sum order, through the net)
 
 
+def test_streaming_1x1_convs_vs_conv_pipe_n256():
+    """The bench batch's ResBlock shortcuts at 32x32 / 16x16 (K = 256..640) on conv1x1_stream_kernel
+    (weights resident in VGPRs, a 4-stage pixel-chunk ring across tiles): the same k order and
+    the same MFMA as conv_pipe, so the forward is bit-identical to conv1x1 = 0; and vs the oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    n = 256
+    gen = torch.Generator().manual_seed(670)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    k1 = [o for o in ops if "conv1x1_stream" in o["kernel"]]
+    assert {o["H"] for o in k1} == {16, 32}, [(o["H"], o["K"], o["kernel"]) for o in ops if o["ks"] == 1]
+
+    def run(v):
+        rt.set_option("conv1x1", v)
+        try:
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("conv1x1", 1)
+
+    st = run(1)
+    assert torch.equal(st, run(0))
+    idx = [0, 255]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    assert _rel_l2(st[idx], ref) < REL_L2_BF16
+
+
 @pytest.mark.parametrize("n", [16, 32])
 def test_small_wide_stats_free_convs_vs_conv_pipe(n):
     """Small batches: the statistics-free convs of 8x8 .. 32x32 images (ResBlock shortcuts, the q|k|v

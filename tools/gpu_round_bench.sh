@@ -9,7 +9,8 @@ tail -3 gpurun_out/$R/gpu_tests.log
 timeout -k 10 600 bash tools/pmc_passes.sh gpurun_out/$R/pmc --n 256 > gpurun_out/$R/pmc.log 2>&1 || { echo pmc_fail; tail -5 gpurun_out/$R/pmc.log; exit 1; }
 python tools/pmc_dispatch.py gpurun_out/$R/pmc > gpurun_out/$R/pmc_dispatch_table.txt || echo dispatch_table_fail
 for k in "conv3x3_gn_p4_kernel<32>" "conv3x3_gn_p4_kernel<16>" "conv3x3_gn_p4_kernel<8>" "conv_small<false>" \
-         "conv_pipe<unsigned short, 2, true>" "attn_mfma_kernel" "gn_apply_kernel" ; do
+         "conv_pipe<unsigned short, 2, true>" "conv1x1_stream_kernel<384, 4>" "conv1x1_stream_kernel<256, 4>" \
+         "conv3x3_gn_p4_kernel<16, 128>" "attn_block_kernel<384>" "gn_apply_kernel" ; do
   f=$(echo "$k" | sed 's/[^A-Za-z0-9]/_/g; s/__*/_/g; s/_$//')
   python tools/pmc_traffic.py gpurun_out/$R/pmc "$k" gpurun_out/$R/pmc_traffic_$f.json > /dev/null || echo "no dispatches: $k"
 done

@@ -9,7 +9,7 @@ for i in 1 2 3 4 5 6; do
   rc=$?
   if grep -q "status=transient\|backing off\|stopped responding while being prepared\|taken away by the GPU service\|no box\|no slot" "$log" && \
      ! grep -q "status=ok\|status=fail" "$log"; then
-    sleep 90; continue
+    if grep -q "backing off" "$log"; then sleep 170; else sleep 90; fi; continue
   fi
   break
 done
