@@ -31,8 +31,9 @@ def main():
     names = {}
     for f in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            # measurement-ablation template arguments default to 0: "<32, 0>" is the shipped "<32>"
-            kn = re.sub(r", 0(, false(, 128)?)?>", ">", r["Kernel_Name"])
+            # the census names drop the default trailing template arguments: "<32, 0, false>" is the
+            # shipped "<32>", "<16, 128, false>" the sub-pixel "<16, 128>"
+            kn = re.sub(r", 0>", ">", re.sub(r", false>", ">", r["Kernel_Name"]))
             if not any(p in kn for p in pats):
                 continue
             k = int(r["Dispatch_Id"])
