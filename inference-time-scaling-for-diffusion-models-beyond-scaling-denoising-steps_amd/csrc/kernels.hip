@@ -1766,7 +1766,6 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   char* halo = tsm + NKS * 12 * 16;                            // [(rpb+2)*(W+2)][PST]
   float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);     // [2 passes][TM_PX][3]
   float* cfl = red + 2 * TM_PX * 3;                            // [C/8][16] this pass's GN coefficients
-  for (int i = tid; i < NKS * 12; i += 256) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
   const int m = lane & 15, kg = lane >> 4;
   int hbase[2];
 #pragma unroll
@@ -1781,8 +1780,18 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   constexpr int TIT = (TM_PX * 3 + 255) / 256;
   float xpre[TIT];
   int tpre = 0;
+  float c1pre = 0.f, c2pre = 0.f, svpre = 0.f;
+  unsigned long long seedpre = 0;
+  long long noffpre = 0;
+  int clippre = -1;
   if (a.step_mode) {
     tpre = *a.tsel;
+    seedpre = a.run->seed;
+    noffpre = a.run->noise_offset;
+    clippre = a.run->clip_at;
+    c1pre = a.coeff1[tpre];
+    c2pre = a.coeff2[tpre];
+    svpre = a.sqrt_var[tpre];
 #pragma unroll
     for (int k = 0; k < TIT; ++k) {
       const int it = tid + 256 * k, opx = it < TM_PX * 3 ? it / 3 : 0, oc = it < TM_PX * 3 ? it - opx * 3 : 0;
@@ -1809,8 +1818,11 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
         v[u] = ok ? *(const u32x4*)(gb + ((size_t)gy * W + gx) * C + ch * 8) : u32x4{0u, 0u, 0u, 0u};
         if (!ok) dst[u] = i < total ? -2 - dst[u] : -1;  // padding: store zeros at -2 - dst
       }
-      if (i0 == 0) {  // the image's GroupNorm coefficients, once in LDS (their loads behind the batch's)
+      if (i0 == 0) {  // the image's GroupNorm coefficients (and, first pass, the weights) into LDS, their
+                      // loads behind the batch's: one memory round trip for all of them
         for (int i = tid; i < cpp * 16; i += 256) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
+        if (pass == 0)
+          for (int i = tid; i < NKS * 12; i += 256) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
         __syncthreads();
       }
 #pragma unroll
@@ -1882,15 +1894,15 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
 #pragma clang fp contract(off)
       const int t = tpre;
       const float xv = xpre[k];
-      const float mean = a.coeff1[t] * xv - a.coeff2[t] * e;
+      const float mean = c1pre * xv - c2pre * e;
       float xn = mean;
       if (t > 0) {
         const float z = a.noise ? a.noise[(size_t)t * a.n * 3 * HW + o]
-                                : philox_normal(a.run->seed, (unsigned)t, (unsigned long long)(a.run->noise_offset + (long long)o));
-        xn = mean + a.sqrt_var[t] * z;
+                                : philox_normal(seedpre, (unsigned)t, (unsigned long long)(noffpre + (long long)o));
+        xn = mean + svpre * z;
       }
       if (xn != xn) atomicOr(a.nan_flag, 1);
-      if (t == a.run->clip_at) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
+      if (t == clippre) xn = fminf(fmaxf(xn, -1.0f), 1.0f);
       a.x[o] = xn;
     }
   }

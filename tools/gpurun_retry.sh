@@ -4,7 +4,7 @@
 # or fail, whatever its exit code -- is returned as is, so a GPU failure is read, not re-run.
 # Usage: tools/gpurun_retry.sh <log> <timeout_s> '<cmd>'
 log=$1; to=$2; cmd=$3
-for i in 1 2 3 4 5 6; do
+for i in 1 2 3 4 5 6 7 8 9 10 11 12; do
   timeout $((to + 900)) /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
   if grep -q "status=transient\|backing off\|stopped responding while being prepared\|taken away by the GPU service\|no box\|no slot" "$log" && \
