@@ -43,6 +43,7 @@ int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_conv1x1 = 1;       // streaming 1x1 kernel for statistics-free 1x1 convs of large pixel counts: 0 off,
                          // 1 on (4-stage ring), 2 on (7-stage ring) ("conv1x1")
+int g_small_8x8 = 1;     // ... and for the 8x8 level's convs when the 128x128 grid under-fills the chip ("small_8x8")
 int g_small_wide = 1;    // ... also for statistics-free convs of larger images (64-pixel tiles inside one image)
                          // whose 128x128 conv_pipe grid under-fills the chip (small batches) ("small_wide")
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
@@ -817,11 +818,11 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
 
 // ---------------------------------------------------------------------------- streaming 1x1
 // Statistics-free 1x1 convs of large pixel counts (the ResBlock shortcuts at the 32x32 / 16x16 levels
-// at N = 256: K = 256..640, Cout = 128 / 256) are HBM streams (~4 bytes of input per MFMA flop-pair
-// ... 128 flops a byte): conv_pipe reloads the weights per 128x128 tile and drains its pipeline per
+// at N = 256: K = 256..640, Cout = 128 / 256) are HBM streams (2 Cout = 256 flops per input byte,
+// below the bf16 ridge): conv_pipe reloads the weights per 128x128 tile and drains its pipeline per
 // tile (~45 % of HBM bandwidth). Here a persistent block keeps one 128-cout tile's weights in
 // VGPRs for the whole launch (wave w: couts 32w..32w+31, all CIN as CIN/16 A fragments straight from
-// the [Cout][K] rows) and streams 128-pixel tiles through a 4-stage global_load_lds ring of 64-channel
+// the [Cout][K] rows) and streams 128-pixel tiles through an NS-stage global_load_lds ring of 64-channel
 // chunks that runs across tile boundaries (the next tile's loads fly during the epilogue); the
 // epilogue rounds acc + bias into an LDS tile and stores it as coalesced 16-B rows. Blocks are dealt
 // XCD-major: the blocks of the cout tiles of one pixel tile share an XCD (its L2 serves the second read).
@@ -3284,8 +3285,11 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
     int S = 1;
     // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
+    // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip)
     const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < 256;
-    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk && (a.Hout * a.Wout <= 16 || wide) &&
+    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256;
+    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
+        (a.Hout * a.Wout <= 16 || wide || small8) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
       const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
       S = std::min(std::min((512 + blocks - 1) / blocks, nK / 2), 16);  // <= 2 combine batches
@@ -3293,7 +3297,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       if (S < 1) S = 1;
     }
     if (g_small_conv && conv_small_ok(a) &&
-        (g_small_conv == 2 || S > 1 || wide ||
+        (g_small_conv == 2 || S > 1 || wide || small8 ||
          (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
       gs.z = S;
       if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);

@@ -567,6 +567,37 @@ def test_streaming_1x1_convs_vs_conv_pipe_n256():
 
 
 @pytest.mark.parametrize("n", [16, 32])
+def test_small_8x8_split_convs_vs_conv_pipe(n):
+    """Small batches: the 8x8 level's plain convs (the 16x16 -> 8x8 DownSample, the shortcuts) whose
+    128x128 conv_pipe grid under-fills the chip run on conv_small's 64x64 whole-image tiles with K split
+    in-launch: deterministic, within 1e-2 relative L2 of conv_pipe (small_8x8 = 0), bf16 bound vs oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(680 + n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    assert any(o["kind"] == "conv" and o["H"] == 8 and "conv_small" in o["kernel"] for o in ops)
+
+    def run(v):
+        rt.set_option("small_8x8", v)
+        try:
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("small_8x8", 1)
+
+    w = run(1)
+    assert torch.equal(w, run(1))
+    p = run(0)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    d, e = _rel_l2(w, p), _rel_l2(w[idx], ref)
+    print(f"n={n}: 8x8 conv_small (split K) vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("n", [16, 32])
 def test_small_wide_stats_free_convs_vs_conv_pipe(n):
     """Small batches: the statistics-free convs of 8x8 .. 32x32 images (ResBlock shortcuts, the q|k|v
     convs) whose 128x128 conv_pipe grid under-fills the chip run on conv_small's 64x64 tiles (inside
