@@ -1251,8 +1251,8 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_m16 = value ? 1 : 0;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "p4_w")) {  // levels conv3x3_gn_p4_kernel takes (bit 0 W = 8, 1 W = 16, 2 W = 32); others p5 / 128-px
-    if (value < 0 || value > 7) return fail(ITSD_ERR_INVALID, "p4_w in [0,7]");
+  if (!std::strcmp(key, "p4_w")) {  // levels conv3x3_gn_p4_kernel takes (bit 0 W = 8, 1 W = 16, 2 W = 32, 3 W = 64); others p5 / 128-px
+    if (value < 0 || value > 15) return fail(ITSD_ERR_INVALID, "p4_w in [0,15]");
     itsd::g_p4_w = value;
     return ITSD_OK;
   }

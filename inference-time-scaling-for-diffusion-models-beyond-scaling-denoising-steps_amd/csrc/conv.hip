@@ -51,7 +51,8 @@ int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whe
 int g_gn_reg = 4;        // the 256-pixel fused GroupNorm conv: 4 = conv3x3_gn_p4_kernel (the only shipped
                          // generation; the superseded 0-3 were deleted in round 4)
 int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel chunk, 0 tap-major (default: 1 measured 2-3 % slower)
-int g_p4_w = 7;          // levels conv3x3_gn_p4_kernel takes: bit 0 W = 8, 1 W = 16, 2 W = 32
+int g_p4_w = 7;          // levels conv3x3_gn_p4_kernel takes: bit 0 W = 8, 1 W = 16, 2 W = 32, 3 W = 64 (off:
+                         // at C4's N = 16, 1 tile a CU, 34.8 vs 33.0 us a launch on p5, profiles/r04/census_c4_p4_64*)
 int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
@@ -1419,6 +1420,9 @@ template <int W> struct GnpCfg;
 template <> struct GnpCfg<32> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<16> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 0; };  // LDS: residual from HBM
+// 64x64 (C4's level 0): 4-row tiles, a 6 x 66-row halo (13 items of 32 rows) -- two halo buffers leave
+// no room for the residual tile, so the register epilogue reads it from HBM as at 8x8
+template <> struct GnpCfg<64> { static constexpr int NSEG = 1, ITEMS = 13, RES = 0; };
 
 
 // ---------------------------------------------------------------------------- persistent, one MFMA wave per SIMD
@@ -3109,7 +3113,8 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout) {
   int segs = 0;
   if (GNW_BN / W <= H) {
     const int THs = GNW_BN / W;
-    if (H % THs == 0 && (THs + 2) * (W + 2) <= GnpCfg<32>::ITEMS * 32) segs = 1;  // p4's halo items
+    const int items = W == 64 ? GnpCfg<64>::ITEMS : GnpCfg<32>::ITEMS;  // p4's halo items (32 rows each)
+    if (H % THs == 0 && (THs + 2) * (W + 2) <= items * 32) segs = 1;
   } else if (GNW_BN == 4 * H * W && (H + 2) * (W + 2) <= GnpCfg<8>::ITEMS * 8) {
     segs = 4;
   }
@@ -3145,7 +3150,8 @@ bool conv_p5_selected(const ConvArgs& a);
 bool conv_p4_selected(const ConvArgs& a) {
   if (!a.gn_coef || conv_p5_selected(a) || !conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
   return g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
-         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
+         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)) ||
+          (a.Wout == 64 && (g_p4_w & 8)));
 }
 
 // A plain (no GroupNorm) 3x3 stride-1 conv on conv3x3_gn_p4_kernel<W, 2>? (the CFG UpSample's conv
@@ -3175,8 +3181,8 @@ bool conv_p4_sub_selected(const ConvArgs& a) {
 bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
   const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
-  // (4x4 and 64x64: no other persistent fused kernel holds them -- p4's 256-pixel halo does not fit at W = 64)
-  return a.Wout == 4 || a.Wout == 64 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
+  // (4x4: no other persistent fused kernel holds it; 64x64 on p5 unless p4_w bit 3 is set)
+  return a.Wout == 4 || (a.Wout == 64 && !(g_p4_w & 8)) || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
 }
 
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
@@ -3233,6 +3239,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
           else if (g_p4_m16 && a.wfrag16 && a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 0, true>), gp, dim3(512), 0, s, a);
           else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p4_kernel<32>, gp, dim3(512), 0, s, a);
           else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p4_kernel<16>, gp, dim3(512), 0, s, a);
+          else if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p4_kernel<64>, gp, dim3(512), 0, s, a);
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }

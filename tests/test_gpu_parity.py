@@ -566,6 +566,39 @@ def test_streaming_1x1_convs_vs_conv_pipe_n256():
     assert _rel_l2(st[idx], ref) < REL_L2_BF16
 
 
+def test_p4_64x64_level_vs_p5_c4_batch():
+    """C4's 64x64 level (Arch A at 64 px, N_local = 16: 256 tiles of 4 rows) on conv3x3_gn_p4_kernel<64>
+    (option p4_w bit 3; residual from HBM in the register epilogue, GroupNorm coefficients from
+    gn_coef) against the shipped p5 kernel: the same k order per accumulator, so bit-identical, and
+    within the bf16 bound of the oracle."""
+    a = ARCH_A64
+    net = _net(a, "bf16")
+    n = 16
+    gen = torch.Generator().manual_seed(690)
+    x = torch.randn(n, 3, 64, 64, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+
+    def run(v):
+        rt.set_option("p4_w", v)
+        try:
+            if v & 8:
+                ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+                assert any("conv3x3_gn_p4_kernel<64>" in o["kernel"] for o in ops if o["H"] == 64)
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("p4_w", 7)
+
+    p4 = run(15)
+    assert torch.equal(p4, run(15))
+    p5 = run(7)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    d, e = _rel_l2(p4, p5), _rel_l2(p4[idx], ref)
+    print(f"64x64 level: p4 vs p5 rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d == 0.0 and e < REL_L2_BF16
+
+
 @pytest.mark.parametrize("n", [16, 32])
 def test_small_8x8_split_convs_vs_conv_pipe(n):
     """Small batches: the 8x8 level's plain convs (the 16x16 -> 8x8 DownSample, the shortcuts) whose
