@@ -20,14 +20,17 @@ Tolerances (measured values are printed; first measurement,
                                                    differ by up to ~1.5 at t = 0)
   C2 per-candidate Oracle-verifier score           |d| <= 1e-3      (measured 1.9e-5 .. 1.1e-4: the
                                                    quantity the search prunes on)
+  C1c MainCondition eval, tiny CFG UNet, fp32      max|d| <= 2e-3    (measured 5.0e-4, guidance w = 1.8)
 """
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
 
 from oracle import ref_cpu as R
 from itsd import entry as E
-from itsd.arch import ARCH_A
+from itsd.arch import ARCH_A, ARCH_TINY_CFG
 from itsd.diffusion import GaussianDiffusionSampler
 from itsd.model import UNet
 from itsd.search import SearchEngine
@@ -39,6 +42,7 @@ pytestmark = pytest.mark.gpu
 FULL_T_FP32_MAXABS = 5e-4
 FULL_T_BF16_REL_L2 = 5e-2
 FULL_T_BF16_SCORE = 1e-3
+FULL_T_FP32_CFG_MAXABS = 2e-3  # guided: eps = 2.8 eps(c) - 1.8 eps(0) amplifies fp32 sum-order drift (measured 5.0e-4)
 
 T = 1000
 PER = 3 * 32 * 32
@@ -128,3 +132,35 @@ def test_C2_bf16_round_T1000_candidates_and_scores_vs_oracle(full_T):
               f"score {float(c2['scores'][i]):.6f} vs oracle {s_ref:.6f} (|d| {ds:.2e})")
         assert rel <= FULL_T_BF16_REL_L2
         assert ds <= FULL_T_BF16_SCORE
+
+
+def test_C1c_main_condition_eval_T1000_fp32_vs_oracle(tmp_path):
+    """MainCondition.py's eval (``TrainCondition.py:118-151`` through ``itsd.entry`` with
+    config/condition_config.yaml keys): the class-block labels of batch_size 10, guided sampling
+    with w = 1.8 and beta_T = 0.028 over T = 1000 steps in fp32 (the tiny CFG UNet: channel 32,
+    channel_mult [1, 2], 1 ResBlock a level, synthetic weights), the saved image against the oracle's
+    full guided loop (``DiffusionCondition.py:79-105``: eps = (1 + w) eps(labels) - w eps(0)) on the
+    same x_T and Philox noise: max|d| <= 2e-3 (measured 5.0e-4; the guidance weights 2.8 / 1.8 amplify the
+    fp32 sum-order differences of the two eps evaluations over the 1000 steps)."""
+    a = dataclasses.replace(ARCH_TINY_CFG, T=1000)
+    cfg = E.load_config(None, ["weights=random", "T=1000", "channel=32", "channel_mult=[1,2]", "num_res_blocks=1",
+                               "batch_size=10", f"sampled_dir={tmp_path}", "seed=11", "nrow=5"],
+                        config_name="condition_config")
+    res = E.run(cfg, condition=True)
+    labels = res["labels"].cpu()
+    assert labels.tolist() == list(range(1, 11))
+    seed = int(res["sampler_seed"])
+    x_T = res["noisy"].cpu()
+    sd = synthetic_state_dict(a, 0)
+    fw = lambda xx, tt, ll: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks, labels=ll, cfg=True)
+    n = x_T.shape[0]
+
+    def noise(step, xx):
+        return torch.stack([R.philox_normal(seed, step, np.arange(j * PER, (j + 1) * PER)).reshape(3, 32, 32)
+                            for j in range(n)])
+
+    with torch.no_grad():
+        ref = R.p_sample_loop(R.cfg_eps(fw, labels, float(cfg["w"])), x_T, R.schedule(1e-4, 0.028, 1000), noise)
+    d = (res["sampled"].cpu() - (ref * 0.5 + 0.5)).abs().max().item()
+    print(f"C1c MainCondition eval, batch 10, T=1000 fp32: x0 max|d| {d:.3e}")
+    assert d <= FULL_T_FP32_CFG_MAXABS
