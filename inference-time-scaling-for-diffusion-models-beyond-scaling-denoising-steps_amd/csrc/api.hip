@@ -47,7 +47,7 @@ bool conv_gn_eligible(int H, int W);
 bool p5_eligible(int H, int W);
 bool conv_p5_selected(const ConvArgs& a);
 bool conv_p4_selected(const ConvArgs& a);
-int conv_gn_wide_segs(int H, int W, int M, int Cout);
+int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
 hipError_t launch_tail_mfma(const TailArgs&, hipStream_t);
@@ -1192,7 +1192,7 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "small_wide")) {  // conv_small for under-filled statistics-free convs of larger images
-    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_wide in [0,1]");
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "small_wide in [0,2]");
     itsd::g_small_wide = value;
     return ITSD_OK;
   }
@@ -1272,7 +1272,7 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p4_plain")) {  // plain 3x3 stride-1 convs on conv3x3_gn_p4_kernel (halo copies the input)
-    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_plain in [0,1]");
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p4_plain in [0,2]");
     itsd::g_p4_plain = value;
     return ITSD_OK;
   }

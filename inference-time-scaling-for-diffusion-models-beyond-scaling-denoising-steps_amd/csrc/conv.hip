@@ -3108,7 +3108,7 @@ bool conv_gn_eligible(int H, int W) {
 
 // Which fused GroupNorm conv launch_conv runs at this shape: 0 = conv3x3_gn_kernel (128 x 128),
 // 1 / 4 = conv3x3_gn_wide_kernel<1 | 4> (256 pixels = rows of one image | four 8x8 images).
-int conv_gn_wide_segs(int H, int W, int M, int Cout) {
+int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false) {
   if (!g_gn_wide || W > GNW_BN || GNW_BN % W || M % GNW_BN) return 0;
   int segs = 0;
   if (GNW_BN / W <= H) {
@@ -3119,7 +3119,7 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout) {
     segs = 4;
   }
   const long long blocks = (long long)(M / GNW_BN) * ((Cout + CONV_BM - 1) / CONV_BM);
-  return segs && (g_gn_wide == 2 || blocks >= 192) ? segs : 0;
+  return segs && (g_gn_wide == 2 || any_tiles || blocks >= 192) ? segs : 0;
 }
 
 
@@ -3160,7 +3160,10 @@ bool conv_p4_plain_selected(const ConvArgs& a) {
   if (!g_p4_plain || a.gn_coef || !a.wfrag || a.ksize != 3 || a.stride != 1 || a.pad != 1 || a.subpix || a.upsample ||
       a.zins || a.vt_out || !a.zero || a.K != 9 * (a.C1 + a.C2) || a.C1 % 64 || a.C2 % 64)
     return false;
-  if (!conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
+  // (down to 128 tiles, half the CUs: the CFG 8x8 UpSample conv at 2N = 64, 145 -> 113 us against conv_pipe,
+  // profiles/r04/census_archC_2N64_p4_plain_128.txt; p4_plain = 2: any tile count)
+  const long long tiles = (a.M % GNW_BN) ? 0 : (long long)(a.M / GNW_BN) * (a.Cout / CONV_BM);
+  if (!conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout, g_p4_plain == 2 || tiles >= 128)) return false;
   return a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.Hin == a.Hout && a.C1 + a.C2 >= 128 &&
          (a.Wout == 32 || a.Wout == 16 || a.Wout == 8);
 }
@@ -3293,7 +3296,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     int S = 1;
     // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
     // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip)
-    const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < 256;
+    const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
     const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256;
     if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
         (a.Hout * a.Wout <= 16 || wide || small8) &&
