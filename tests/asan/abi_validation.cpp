@@ -61,7 +61,7 @@ int main() {
   expect("set_option conv_wide=1 (removed)", itsd_set_option("conv_wide", 1), ITSD_ERR_INVALID);
   expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
-  expect("set_option p4_w=8", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
+  expect("set_option p4_w=16", itsd_set_option("p4_w", 16), ITSD_ERR_INVALID);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it
     std::string k(4096, 'k');
