@@ -1186,6 +1186,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_conv1x1 = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "tail_px")) {  // tail_mfma_kernel output pixels a block
+    if (value != 64 && value != 128) return fail(ITSD_ERR_INVALID, "tail_px in {64, 128}");
+    itsd::g_tail_px = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "small_8x8")) {  // conv_small (split K) for under-filled 8x8-level convs
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_8x8 in [0,1]");
     itsd::g_small_8x8 = value;

@@ -22,6 +22,7 @@ extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide"
 extern int g_splitk_inl;     // conv_pipe split-K combined in-launch: 0 off (second launch), 1 on (itsd_set_option "splitk_inl")
 extern int g_p4_plain;      // plain (no GroupNorm) 3x3 stride-1 convs on conv3x3_gn_p4_kernel<W, 2>: 0 off, 1 on (itsd_set_option "p4_plain")
 extern int g_conv1x1;        // streaming 1x1 conv kernel: 0 off, 1 on ("conv1x1")
+extern int g_tail_px;        // tail_mfma_kernel output pixels a block: 128 or 64 ("tail_px")
 extern int g_small_8x8;      // conv_small (split K) for under-filled 8x8-level convs ("small_8x8")
 extern int g_small_wide;     // conv_small for under-filled statistics-free convs of larger images ("small_wide")
 extern int g_attn_wide_nq;   // its query groups a block: 0 auto, 1 / 2 forced ("attn_wide_nq")

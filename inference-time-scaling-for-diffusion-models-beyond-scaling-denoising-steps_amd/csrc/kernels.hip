@@ -1188,21 +1188,27 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
       mx = fmaxf(mx, s[r]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    // lazy rescale: the running max moves (and O, l are rescaled) only when some query of the wave
+    // gains more than 8 (log2 units) on it; otherwise P = 2^(s - m) <= 256 against the stale max,
+    // the same quotient O / l (wave-uniform branch; the first tile always takes it, m = -inf)
+    if (__ballot(mx > m + 8.0f) != 0ull) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+    }
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s[r] = exp2f(s[r] - mn);
+      s[r] = exp2f(s[r] - m);
       rs += s[r];
     }
     rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+    l += rs;
     const bf16_t* vs = Vs[buf] + rl * VP + 8 * hh;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -1318,21 +1324,27 @@ __global__ __launch_bounds__(256 * NQ) void attn_cs_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    // lazy rescale: the running max moves (and O, l are rescaled) only when some query of the wave
+    // gains more than 8 (log2 units) on it; otherwise P = 2^(s - m) <= 256 against the stale max,
+    // the same quotient O / l (wave-uniform branch; the first tile always takes it, m = -inf)
+    if (__ballot(mx > m + 8.0f) != 0ull) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+    }
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s[r] = exp2f(s[r] - mn);
+      s[r] = exp2f(s[r] - m);
       rs += s[r];
     }
     rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[cb][r] *= alpha;
+    l += rs;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       bf16x8 bp;
@@ -1755,7 +1767,9 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 // (HBM latency once per batch, not per chunk). Each wave owns 2 x 16 pixels:
 // eps[pixel][co] = sum_k patch[pixel][k] W[co][k] on v_mfma_f32_16x16x32_bf16
 // (k = tap*C + ci; 9C/32 k-steps; B columns 3..15 are zero).
-constexpr int TM_PX = 128;  // output pixels per block
+// TM_PX output pixels per block: 128, or 64 (option "tail_px": a smaller halo, 3 blocks a CU)
+int g_tail_px = 128;
+template <int TM_PX>
 __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   const int C = a.C, W = a.W, H = a.H, HW = H * W;
@@ -1852,6 +1866,7 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     __syncthreads();
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int cpt = C / 32;
+    if (wid * 32 < TM_PX) {  // (TM_PX = 64: waves 0, 1 own the block's pixels)
 #pragma unroll 4
     for (int ks = 0; ks < NKS; ++ks) {
       const int tap = ks / cpt, ci0 = (ks - tap * cpt) * 32;
@@ -1870,6 +1885,7 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
       for (int gi = 0; gi < 2; ++gi)
 #pragma unroll
         for (int i = 0; i < 4; ++i) red[(pass * TM_PX + wid * 32 + gi * 16 + 4 * kg + i) * 3 + m] = acc[gi][i];
+    }
     }
   }
   __syncthreads();
@@ -1908,27 +1924,32 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   }
 }
 
-size_t tail_mfma_smem(int H, int W, int C) {
-  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(TM_PX / W + 2) * (W + 2) * (2 * C + 16) + 2 * TM_PX * 3 * 4 +
+static size_t tail_mfma_smem_px(int px, int H, int W, int C) {
+  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(px / W + 2) * (W + 2) * (2 * C + 16) + 2 * px * 3 * 4 +
          (size_t)C * 2 * 4;
 }
-
-bool tail_mfma_ok(int H, int W, int C) {
-  return W <= TM_PX && TM_PX % W == 0 && TM_PX / W <= H && H % (TM_PX / W) == 0 && C % 32 == 0 &&
-         tail_mfma_smem(H, W, C) <= 160 * 1024;
+static bool tail_mfma_ok_px(int px, int H, int W, int C) {
+  return W <= px && px % W == 0 && px / W <= H && H % (px / W) == 0 && C % 32 == 0 &&
+         tail_mfma_smem_px(px, H, W, C) <= 160 * 1024;
 }
+size_t tail_mfma_smem(int H, int W, int C) { return tail_mfma_smem_px(128, H, W, C); }
+bool tail_mfma_ok(int H, int W, int C) { return tail_mfma_ok_px(128, H, W, C); }
 
 hipError_t launch_tail_mfma(const TailArgs& a, hipStream_t s) {
   if (!a.coef || !a.wmf || !tail_mfma_ok(a.H, a.W, a.C)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)tail_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)tail_mfma_kernel<128>, (const void*)tail_mfma_kernel<64>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
-  ITSD_LAUNCH(tail_mfma_kernel, dim3(a.n * (a.H / (TM_PX / a.W))), dim3(256), tail_mfma_smem(a.H, a.W, a.C), s,
-                     a);
+  if (g_tail_px == 64 && tail_mfma_ok_px(64, a.H, a.W, a.C))
+    ITSD_LAUNCH(tail_mfma_kernel<64>, dim3(a.n * (a.H / (64 / a.W))), dim3(256), tail_mfma_smem_px(64, a.H, a.W, a.C), s, a);
+  else
+    ITSD_LAUNCH(tail_mfma_kernel<128>, dim3(a.n * (a.H / (128 / a.W))), dim3(256), tail_mfma_smem_px(128, a.H, a.W, a.C),
+                s, a);
   return hipGetLastError();
 }
 

@@ -537,6 +537,25 @@ def test_subpixel_split_k_vs_unsplit(arch, n):
     assert d < 1e-2 and e < REL_L2_BF16  # (measured 5.7e-3 / 7.8e-3: one conv's sum order, through the net)
 
 
+@pytest.mark.parametrize("n", [8, 256])
+def test_tail_64px_blocks_bit_identical(n):
+    """tail_mfma_kernel with 64-pixel blocks (tail_px = 64: a 4-row halo, waves 0-1 run the MFMAs) computes
+    every output exactly as the 128-pixel blocks: sampler steps bit-identical (Philox mode, bf16)."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, a.T)
+    x = torch.randn(n, 3, 32, 32, generator=torch.Generator().manual_seed(700 + n)).cuda()
+
+    def run(px):
+        rt.set_option("tail_px", px)
+        try:
+            return smp.run(x.clone(), t_begin=999, t_end=996, seed=3).cpu()
+        finally:
+            rt.set_option("tail_px", 128)
+
+    assert torch.equal(run(64), run(128))
+
+
 def test_streaming_1x1_convs_vs_conv_pipe_n256():
     """The bench batch's ResBlock shortcuts at 32x32 / 16x16 (K = 256..640) on conv1x1_stream_kernel
     (weights resident in VGPRs, a 4-stage pixel-chunk ring across tiles): the same k order and

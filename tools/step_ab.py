@@ -18,6 +18,13 @@ from itsd.diffusion import GaussianDiffusionSampler
 from itsd.model import UNet
 
 
+# the shipped value of every option a variant may touch (a variant's keys are reset to these after it runs)
+DEFAULTS = {"gn_fold": 1, "p5": 1, "p5_split": 0, "splitk_inl": 1, "p4_plain": 1, "splitk": 1, "attn_split": 1,
+            "p4_sub": 1, "gn_wide": 1, "small_conv": 1, "conv_variant": 2, "small_wide": 1, "small_8x8": 1,
+            "subpix_split": 1, "conv1x1": 1, "tail_px": 128, "attn_wide": 1, "attn_wide_nq": 1, "p4_w": 7,
+            "attn_fuse": 1, "fuse_gn": 1, "conv_dbg": 0, "small_korder": 0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=32)
@@ -50,8 +57,7 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
             res[v].append(ms)
             for k in opts:  # back to the default of each option touched
-                rt.set_option(k, {"gn_fold": 1, "p5": 1, "p5_split": 0, "splitk_inl": 1, "p4_plain": 1, "splitk": 1,
-                                 "attn_split": 1, "p4_sub": 1, "gn_wide": 1, "small_conv": 1, "conv_variant": 2}.get(k, 0))
+                rt.set_option(k, DEFAULTS[k])
             print(f"round {r} {v}: {ms:.4f} ms/step", flush=True)
     for v in variants:
         print(f"{v}: best {min(res[v]):.4f} ms/step  ({args.n * 1000 / min(res[v]) / 1000 * 1000 / 1000:.2f} cand/s at T=1000)")
