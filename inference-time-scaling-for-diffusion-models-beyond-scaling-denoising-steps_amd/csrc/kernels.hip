@@ -1240,27 +1240,28 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
 #undef ITSD_FLASH_LSTORE
 }
 
-// Channel-split attention for wide channels (C = 256 .. 512, S % 32 == 0: Arch A's 16x16 level at
-// 64 px (S = 256, C = 384), the CFG model's 16x16 level (S = 256, C = 512)), where one wave cannot hold
-// q and O for all C channels. A block takes 32 queries; wave w owns channels [w C/4, (w+1) C/4) for
+// Channel-split attention for wide channels (C = 256 .. 1024, S % 64 == 0: Arch A's 16x16 level at
+// 64 px (S = 256, C = 384), the CFG model's 16x16 level (S = 256, C = 512) and 8x8 level (S = 64,
+// C = 1024, NW = 8 waves a query group)), where one wave cannot hold q and O for all C channels.
+// A block takes 32 queries per group; wave w owns channels [w C/NW, (w+1) C/NW) for
 // BOTH products, so every K / V byte is read once per block with no LDS staging:
 //  - per 32-key tile each wave computes a partial s^T = K_w q_w^T over its channels (C/64 MFMAs,
 //    K fragments prefetched a tile ahead), writes it to LDS, and after one barrier every wave sums
-//    the 4 partials in wave order (identical scores in all waves: deterministic), runs the online
+//    the NW partials in wave order (identical scores in all waves: deterministic), runs the online
 //    softmax and O_w^T += V_w^T P^T on its own C/128 channel blocks (V^T fragments prefetched a tile
 //    ahead, the flash kernel's key permutation);
 //  - the partial-score buffer is double-buffered by tile parity: one barrier a tile.
-template <int C, int NQ>
-__global__ __launch_bounds__(256 * NQ) void attn_cs_kernel(AttnArgs a) {
-  constexpr int CQ = C / 4, QS = CQ / 16, CB = CQ / 32, C3 = 3 * C;
+template <int C, int NQ, int NW = 4>
+__global__ __launch_bounds__(64 * NW * NQ) void attn_cs_kernel(AttnArgs a) {
+  constexpr int CQ = C / NW, QS = CQ / 16, CB = CQ / 32, C3 = 3 * C;
   static_assert(CQ % 32 == 0, "whole 32-channel blocks a wave");
   // [tile parity][query group][wave of the group][r / 4][lane][r % 4]
-  __shared__ __attribute__((aligned(16))) float Sp[2][NQ][4][4][64][4];
+  __shared__ __attribute__((aligned(16))) float Sp[2][NQ][NW][4][64][4];
   const int S = a.S, QT = S / (32 * NQ);
   const int nb = gridDim.x, bx = blockIdx.x;
   const int L = (nb & 7) ? bx : (bx & 7) * (nb >> 3) + (bx >> 3);  // XCD-major: an image's tiles on one XCD
   const int img = L / QT, qt = L - img * QT;
-  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3, qg = tid >> 8, rl = lane & 31, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) % NW, qg = (tid >> 6) / NW, rl = lane & 31, hh = lane >> 5;
   const int q = (qt * NQ + qg) * 32 + rl, ch0 = wid * CQ;
   const bf16_t* base = (const bf16_t*)a.qkv + (size_t)img * S * C3;
   const bf16_t* vt = (const bf16_t*)a.vt + (size_t)img * C * S;
@@ -1315,7 +1316,7 @@ __global__ __launch_bounds__(256 * NQ) void attn_cs_kernel(AttnArgs a) {
     for (int g = 0; g < 4; ++g) {
       f32x4 v = *(const f32x4*)&Sp[par][qg][0][g][lane][0];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) v += *(const f32x4*)&Sp[par][qg][w][g][lane][0];
+      for (int w = 1; w < NW; ++w) v += *(const f32x4*)&Sp[par][qg][w][g][lane][0];
 #pragma unroll
       for (int e = 0; e < 4; ++e) s[4 * g + e] = v[e] * sl2;
     }
@@ -1369,7 +1370,7 @@ __global__ __launch_bounds__(256 * NQ) void attn_cs_kernel(AttnArgs a) {
       *(uint2*)(out + c) = w2;
     }
 }
-bool attn_cs_ok(int S, int C) { return S % 64 == 0 && (C == 256 || C == 384 || C == 512); }
+bool attn_cs_ok(int S, int C) { return S % 64 == 0 && (C == 256 || C == 384 || C == 512 || C == 1024); }
 
 bool attn_flash_ok(int S, int C) { return S % 32 == 0 && (C == 64 || C == 128 || C == 256); }
 
@@ -1382,6 +1383,11 @@ template <typename T>
 hipError_t launch_attn(const AttnArgs& a, int n, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     // channel-split attention: auto (g_attn_wide = 1) for C >= 384 at S >= 256; 2 = wherever it applies
+    // (C = 1024, the CFG 8x8 level at S = 64: 8 waves of 128 channels a query group)
+    if (a.vt && g_attn_wide && attn_cs_ok(a.S, a.C) && a.C == 1024) {
+      ITSD_LAUNCH((attn_cs_kernel<1024, 1, 8>), dim3((unsigned)((a.S / 32) * n)), dim3(512), 0, s, a);
+      return hipGetLastError();
+    }
     if (a.vt && g_attn_wide && attn_cs_ok(a.S, a.C) && (g_attn_wide == 2 || (a.C >= 384 && a.S >= 256))) {
       // 64 queries (two groups of 4 waves) a block; 32 when the query tiles of 64 leave CUs idle
       if (g_attn_wide_nq == 2 || (g_attn_wide_nq == 0 && (long long)(a.S / 64) * n >= g_num_cus)) {

@@ -161,7 +161,7 @@ int main() {
   expect("attention bf16+vt S=20", itsd_attention(f, f, f, 1, 20, 64, 1, nullptr), ITSD_ERR_INVALID);
   expect("attention bf16+vt C=96", itsd_attention(f, f, f, 1, 16, 96, 1, nullptr), ITSD_ERR_INVALID);
   expect("attention wide S=1056 C=512 (S % 64)", itsd_attention(f, f, f, 1, 1056, 512, 1, nullptr), ITSD_ERR_INVALID);
-  expect("attention S=1024 C=1024", itsd_attention(f, f, f, 1, 1024, 1024, 1, nullptr), ITSD_ERR_INVALID);
+  expect("attention S=1024 C=768", itsd_attention(f, f, f, 1, 1024, 768, 1, nullptr), ITSD_ERR_INVALID);
   expect("attention fp32 C=6", itsd_attention(f, nullptr, f, 1, 16, 6, 0, nullptr), ITSD_ERR_INVALID);
 
   // ---- itsd_noise

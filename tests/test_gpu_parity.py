@@ -287,6 +287,9 @@ def _attn_ref(qkv):
     (1, 4096, 256, torch.bfloat16, True, 1),  # Arch A at 256 px, level 2: flash kernel
     (3, 320, 64, torch.bfloat16, True, 1),    # flash kernel, ragged last query tile
     (2, 64, 384, torch.bfloat16, True, 1),    # Arch A level 2: whole-row MFMA kernel
+    (2, 64, 1024, torch.bfloat16, True, 1),   # C3 level 2: channel-split kernel, 8 waves a query group
+    (3, 128, 1024, torch.bfloat16, True, 1),  # the same, 4 key tiles
+    (2, 64, 1024, torch.bfloat16, True, 0),   # C3 level 2 on the whole-row MFMA kernel
     (2, 16, 1024, torch.bfloat16, True, 1),   # C3 level 3
     (2, 4, 512, torch.bfloat16, False, 1),    # C3 level 4: VALU kernel
     (2, 1024, 128, torch.float32, False, 1),  # parity mode
