@@ -881,6 +881,7 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
       a.M = c.nb * in.H * in.W;
       a.ksize = o.subpix == 2 ? o.ksize : 2; a.pad = o.subpix == 2 ? o.pad : 0; a.upsample = 0; a.zins = 0;
       a.K = a.ksize * a.ksize * (a.C1 + a.C2);
+      a.tap_live = o.subpix == 2 && a.ksize == 3 && itsd::g_convt_prune;  // (p4: skip the zero taps)
     }
     if (o.coef != SIZE_MAX) {
       if (!u->bf16 || o.ksize != 3 || o.stride != 1 || o.pad != 1 || o.upsample || o.zins ||
@@ -1269,6 +1270,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p4_sub")) {  // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form: 0 off, 1 on
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_sub in [0,1]");
     itsd::g_p4_sub = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "convt_prune")) {  // ConvTranspose2d sub-pixel phases skip their all-zero taps (p4 / conv_pipe)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "convt_prune in [0,1]");
+    itsd::g_convt_prune = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "subpix_split")) {  // under-filled sub-pixel conv_pipe launches split K in-launch

@@ -27,6 +27,7 @@ extern int g_small_8x8;      // conv_small (split K) for under-filled 8x8-level 
 extern int g_small_wide;     // conv_small for under-filled statistics-free convs of larger images ("small_wide")
 extern int g_attn_wide_nq;   // its query groups a block: 0 auto, 1 / 2 forced ("attn_wide_nq")
 extern int g_attn_wide;      // channel-split attention: 0 off, 1 auto, 2 wherever it applies ("attn_wide")
+extern int g_convt_prune;  // ConvTranspose2d sub-pixel phases skip their all-zero taps: 0 off, 1 on ("convt_prune")
 extern int g_subpix_split;  // under-filled sub-pixel conv_pipe launches split K in-launch: 0 off, 1 on ("subpix_split")
 extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
@@ -145,6 +146,8 @@ struct ConvArgs {
                                      // (grid.z = phase py*2+px): Hout/Wout/M/ksize/K describe the
                                      // input-grid GEMM; output rows are (2i+py, 2j+px) of a 2x grid
   int dbg;                           // g_conv_dbg (measurements only)
+  int tap_live;                      // subpix 2 on conv3x3_gn_p4_kernel: skip each phase's all-zero taps
+                                     // (conv_pipe runs all 9: measured no faster with live taps)
   // conv3x3_gn_p5_kernel (the fused conv of the 8x8 / 4x4 levels): K split into ksplit slices
   // (>= 1) combined in-launch by the last-arriving slice of each (tile, MFMA wave); tickets[]
   // are zero between launches (zeroed at create, reset by each last arriver)

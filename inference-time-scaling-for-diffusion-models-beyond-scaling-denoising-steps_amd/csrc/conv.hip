@@ -57,6 +57,7 @@ int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
+int g_convt_prune = 1;    // ConvTranspose2d sub-pixel phases skip their all-zero taps (itsd_set_option "convt_prune")
 int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
@@ -1463,7 +1464,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
-  constexpr int RING = (AB & 64) ? 4 : (SUB4 ? 4 : P4_RING), BD = (AB & 32) ? P4_BD + 1 : P4_BD;
+  // (sub-pixel forms: 4 slots, dividing every phase's k-step count: 16, or 36 / 24 / 24 / 16 live)
+  constexpr int RING = ((AB & 64) || SUB) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
   static_assert(KST % RING == 0, "ring slots repeat per chunk");
   static_assert(!(SUB && M16), "the sub-pixel form runs the 32x32x16 MFMA path");
   // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]
@@ -1488,10 +1490,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int ntiles = (int)(((long long)(b + 1) * NT) / G) - tb0;
   const int nstages = ntiles * ncc;
   // tile t = ((phase * nPT) + pixel tile) * nTC + cout tile (SUB: phase slowest, so a block's contiguous
-  // range keeps one phase's weights)
-  auto tile_p = [&](int k) { return (SUB ? ((tb0 + k) / nTC) % nPT : (tb0 + k) / nTC) * GNW_BN; };
-  auto tile_c = [&](int k) { return ((tb0 + k) % nTC) * CONV_BM; };
-  auto tile_ph = [&](int k) { return SUB ? (tb0 + k) / (nTC * nPT) : 0; };
+  // range keeps one phase's weights). ConvTranspose2d phases with tap_live cost 9 / 6 / 6 / 4 taps: the
+  // first half of the sequence alternates phases 0 and 3 (same pixel / cout tile), the second 1 and 2, so
+  // that a block's contiguous pair of tiles costs 13 or 12 taps (phase-major: 18 .. 8)
+  constexpr bool CT = SUB && !SUB4;
+  const int Q = nPT * nTC;
+  auto tile_r = [&](int k) -> int {  // (SUB: the tile within its phase)
+    const int t = tb0 + k;
+    if constexpr (!SUB) return t;
+    if (CT && a.tap_live) return (t - (t >= 2 * Q ? 2 * Q : 0)) >> 1;
+    return t % Q;
+  };
+  auto tile_p = [&](int k) { return (tile_r(k) / nTC) * GNW_BN; };
+  auto tile_c = [&](int k) { return (tile_r(k) % nTC) * CONV_BM; };
+  auto tile_ph = [&](int k) -> int {
+    const int t = tb0 + k;
+    if constexpr (!SUB) return 0;
+    if (CT && a.tap_live) return t >= 2 * Q ? 1 + ((t - 2 * Q) & 1) : 3 * (t & 1);
+    return t / Q;
+  };
   // SUB: output NHWC row of input-grid pixel p of phase ph: (img, 2i + py, 2j + px) of the 2x grid
   auto orow = [&](int p, int ph) -> size_t {
     if constexpr (!SUB) return (size_t)p;
@@ -1699,8 +1716,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         dst[1] = *(const u32x4*)(base + ablk + off);
       }
     };
+    // ConvTranspose2d phases with tap_live: a chunk runs only its phase's live taps; the A prefetch that
+    // crosses into the next chunk / tile starts at that chunk's first live tap (tap0_off)
+    auto tap0_off = [&](int k) -> size_t {
+      if constexpr (CT) {
+        if (a.tap_live) {
+          const int ph = tile_ph(k);
+          return (size_t)(((ph >> 1) * 3 + (ph & 1)) * kpt) * 1024;
+        }
+      }
+      return 0;
+    };
     {
-      const char* ab0 = abase_of(0);
+      const char* ab0 = abase_of(0) + tap0_off(0);
 #pragma unroll
       for (int s0 = 0; s0 < RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
     }
@@ -1725,57 +1753,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     for (int k = 0; k < ntiles; ++k) {
       const int tileP = tile_p(k), tileC = tile_c(k), tph = tile_ph(k);
       const char* ab = abase_of(k);
-      const char* abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
+      const char* abn = k + 1 < ntiles ? abase_of(k + 1) + tap0_off(k + 1) : ab;
+      const size_t t0k = tap0_off(k);
       for (int cc = 0; cc < ncc; ++cc, ++q) {
         const char* hcur = smem + (q & 1) * HALO;
-        const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 4 * 1024 : (k + 1 < ntiles ? abn : ab);
+        const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 4 * 1024 + t0k : (k + 1 < ntiles ? abn : ab);
         const char* cb = ab + (size_t)cc * 4 * 1024;
         STAMP(c0);
-        // 36 k-steps (9 taps x 4); B fragments two k-steps ahead (three buffers), across tap
-        // boundaries; fragment j of step s at byte (h * 128 + ((hh ^ sw(h)) << 4)) ^ (kk << 5)
-        // B fragment j of k-step st: byte (h * 128 + ((hh ^ sw(h)) << 4)) ^ (kk << 5), h = the
-        // pixel's halo row for tap st / 4, kk = st % 4: the tap's 4 row addresses are rebuilt (from
-        // an opaque copy, so they are not hoisted out of the chunk loop: 36 registers) every 4th
-        // read and XORed per k-step
-        int tb[4];
-        bf16x8 fb[BD][4];
-        auto rd = [&](int st, int buf) __attribute__((always_inline)) {
-          if ((st & 3) == 0) {
-            const int tap = st >> 2;
-            // SUB4: tap (dy, dx) of phase (py, px) reads input offset (dy + py - 1, dx + px - 1)
-            const int ky = SUB4 ? (tap >> 1) + (tph >> 1) : tap / 3, kx = SUB4 ? (tap & 1) + (tph & 1) : tap - (tap / 3) * 3;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              int h = hb[j] + ky * W2 + kx;
-              asm volatile("" : "+v"(h));
-              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if constexpr ((AB & 16) != 0) fb[buf][j] = bf16x8{(short)(st + j), 0, 0, 0, 0, 0, 0, 1};
-            else fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 3) << 5)));
-          }
-        };
-#pragma unroll
-        for (int s0 = 0; s0 < BD - 1; ++s0) rd(s0, s0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int step = 0; step < KST; ++step) {
-          const int pf = step + RING - 1;
-          if (pf < KST) load_a(cb, pf, ra[pf % RING]);
-          else load_a(nb, pf - KST, ra[pf % RING]);
-          if (step + BD - 1 < KST) rd(step + BD - 1, (step + BD - 1) % BD);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % RING][i]);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if constexpr ((AB & 1) != 0) acc[i][j][0] += __builtin_bit_cast(float, (uint32_t)fb[step % BD][j][0] << 16) + (float)af[0];
-              else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % BD][j], acc[i][j], 0, 0, 0);
-          }
-          // the step's A loads, B reads and address VALU spread over its 8 MFMA gaps (measured against all of
-          // them ahead of the MFMAs in one gap: 32x32 -1 %, 16x16 -3 %, 8x8 -1.5 %, profiles/r03b/p4_sgb_ab.txt)
+        // the step's A loads, B reads and address VALU spread over its 8 MFMA gaps (measured against all of
+        // them ahead of the MFMAs in one gap: 32x32 -1 %, 16x16 -3 %, 8x8 -1.5 %, profiles/r03b/p4_sgb_ab.txt)
+        auto step_sched = [&]() __attribute__((always_inline)) {
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1794,6 +1781,87 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
             __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
+        };
+        auto mfma_step = [&](const u32x4 (&af2)[2], const bf16x8 (&fbs)[4]) __attribute__((always_inline)) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const bf16x8 af = __builtin_bit_cast(bf16x8, af2[i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if constexpr ((AB & 1) != 0) acc[i][j][0] += __builtin_bit_cast(float, (uint32_t)fbs[j][0] << 16) + (float)af[0];
+              else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fbs[j], acc[i][j], 0, 0, 0);
+          }
+        };
+        // B fragment j of k-step kk of the tap at halo offset (ky, kx): byte (h * 128 + ((hh ^ sw(h)) << 4))
+        // ^ (kk << 5), h = the pixel's halo row for the tap: the tap's 4 row addresses are rebuilt (from an
+        // opaque copy, so they are not hoisted out of the chunk loop: 36 registers) at its first k-step
+        int tb[4];
+        bf16x8 fb[BD][4];
+        auto rd_tap = [&](int ky, int kx, int kk, int buf) __attribute__((always_inline)) {
+          if (kk == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              int h = hb[j] + ky * W2 + kx;
+              asm volatile("" : "+v"(h));
+              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr ((AB & 16) != 0) fb[buf][j] = bf16x8{(short)(kk + j), 0, 0, 0, 0, 0, 0, 1};
+            else fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ (kk << 5)));
+          }
+        };
+        if constexpr (CT) {
+          static_assert(RING == 4 && BD == 2, "one tap's 4 k-steps per ring turn");
+          // ConvTranspose2d phases: a run-time loop over the phase's live taps (window rows ry..2 x
+          // columns rx..2 with tap_live; all 9 otherwise), 4 unrolled k-steps a tap: step kk of every tap
+          // uses ring slot kk and B buffer kk & 1; the A prefetch 3 steps ahead reaches into the next
+          // live tap (or the next chunk, nb, at the last one)
+          const int ry = a.tap_live ? (tph >> 1) : 0, rx = a.tap_live ? (tph & 1) : 0;
+          const int ntl = (3 - ry) * (3 - rx);
+          int ky = ry, kx = rx;
+          rd_tap(ky, kx, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          for (int ti = 0; ti < ntl; ++ti) {
+            const bool last = ti + 1 == ntl;
+            const int nky = kx == 2 ? ky + 1 : ky, nkx = kx == 2 ? rx : kx + 1;
+            const int rky = last ? ky : nky, rkx = last ? kx : nkx;  // (the last tap re-reads its own rows)
+            const char* tcur = cb + (size_t)((ky * 3 + kx) * kpt) * 1024;
+            const char* tnxt = last ? nb : cb + (size_t)((nky * 3 + nkx) * kpt) * 1024;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+              if (kk == 0) load_a(tcur, 3, ra[3]);
+              else load_a(tnxt, kk - 1, ra[kk - 1]);
+              if (kk < 3) rd_tap(ky, kx, kk + 1, (kk + 1) & 1);
+              else rd_tap(rky, rkx, 0, 0);
+              mfma_step(ra[kk], fb[kk & 1]);
+              step_sched();
+            }
+            ky = nky;
+            kx = nkx;
+          }
+        } else {
+          // 36 (9 taps x 4) or 16 (4 taps x 4) k-steps, fully unrolled; B fragments BD - 1 k-steps ahead,
+          // across tap boundaries
+          auto rd = [&](int st, int buf) __attribute__((always_inline)) {
+            const int tap = st >> 2;
+            // SUB4: tap (dy, dx) of phase (py, px) reads input offset (dy + py - 1, dx + px - 1)
+            const int ky = SUB4 ? (tap >> 1) + (tph >> 1) : tap / 3, kx = SUB4 ? (tap & 1) + (tph & 1) : tap - (tap / 3) * 3;
+            rd_tap(ky, kx, st & 3, buf);
+          };
+#pragma unroll
+          for (int s0 = 0; s0 < BD - 1; ++s0) rd(s0, s0);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int step = 0; step < KST; ++step) {
+            const int pf = step + RING - 1;
+            if (pf < KST) load_a(cb, pf, ra[pf % RING]);
+            else load_a(nb, pf - KST, ra[pf % RING]);
+            if (step + BD - 1 < KST) rd(step + BD - 1, (step + BD - 1) % BD);
+            mfma_step(ra[step % RING], fb[step % BD]);
+            step_sched();
+          }
         }
         STAMP(c1);
         STAMP_ADD(0, c1 - c0);
@@ -3295,9 +3363,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
     int S = 1;
     // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
-    // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip)
+    // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip; not
+    // for K >= 7168: the CFG's merged 5x5 DownSample into 8x8, K = 12800 at 2N = 64, measured 156 us on
+    // conv_small's 64x64 tiles vs 97 us on the 128-tile pipe, profiles/r04/census_archC_2N64_small8_k.txt)
     const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
-    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256;
+    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256 &&
+                        a.K < 7168;
     if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
         (a.Hout * a.Wout <= 16 || wide || small8) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {

@@ -509,6 +509,40 @@ def test_p4_subpixel_convtranspose_vs_conv_pipe_cfg():
     assert d < 1e-2 and e < REL_L2_BF16
 
 
+def test_convtranspose_live_taps_vs_all_taps():
+    """The CFG UpSample's ConvTranspose2d(5, 2, 2, 1) phases on conv3x3_gn_p4_kernel (8x8 -> 16x16 and
+    16x16 -> 32x32 at 2N = 64) run only the taps of their 3x3 window that have a kernel tap (9 / 6 / 6 / 4:
+    the others' weights are zero, pack_convt_subpix) and deal the phase tiles in cost-balanced pairs. A
+    tile sums the same nonzero products in the same order, so the forward is bit-identical to the all-taps
+    launch (convt_prune = 0), and within the bf16 bound of the oracle."""
+    a = ARCH_C
+    net = _net(a, "bf16")
+    n = 64
+    gen = torch.Generator().manual_seed(660)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, a.T, (n,), generator=gen)
+    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n // 2, dtype=torch.long)])
+    x, t, lb = xc.cuda(), tc.cuda(), lab.cuda()
+    ops = net.native(n).profile_ops(x, t.to(torch.int32))
+    assert sum("384>" in o["kernel"] for o in ops) == 2, [o["kernel"] for o in ops]
+
+    def run(prune):
+        rt.set_option("convt_prune", prune)
+        try:
+            return net(x, t, lb).float().cpu()
+        finally:
+            rt.set_option("convt_prune", 1)
+
+    live = run(1)
+    assert torch.equal(live, run(0))
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
+    e = _rel_l2(live[idx], ref)
+    print(f"CFG 2N=64: live-tap ConvTranspose bit-identical to all taps; vs oracle {e:.2e}")
+    assert e < REL_L2_BF16
+
+
 @pytest.mark.parametrize("arch,n", [(ARCH_C, 64), (ARCH_A, 8)])
 def test_subpixel_split_k_vs_unsplit(arch, n):
     """Under-filled sub-pixel conv_pipe launches (the CFG ConvTranspose2d from the 2x2 grid at 2N = 64:
