@@ -397,6 +397,8 @@ struct TileId {
 // share a cout tile (its weights) then share one L2 -- at the 8x8 / 4x4 levels the
 // weight matrices (up to 9.4 MB) do not fit one 4 MB L2 if every XCD needs all of them.
 // Speed only: correctness never depends on placement.
+// (A cout-major order -- an XCD's range = a band of cout tiles x every pixel tile -- for the weight-heavy
+// CFG 4x4 / 8x8 conv_pipe launches measured no faster: profiles/r04/census_archC_2N64_wmajor.txt)
 __device__ __forceinline__ TileId tile_of_block(bool pixel_major = false) {
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   const int B = gx * gy * gz;
@@ -3420,7 +3422,11 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
       if (S > 1) grid.z = 4 * S;
     }
-    ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+    // (conv_variant 3 / 0: 3- / 4-stage rings at one block a CU, measured 8-30 % slower here,
+    // profiles/r04/census_archC_2N64_conv_variant*.txt)
+    if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
+    else if (v == 0) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
+    else ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
   ConvArgs b = a;  // (conv_pipe's split-K: in-launch combine unless the tiles outnumber the tickets)
