@@ -1320,7 +1320,7 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_attn_wide_nq = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "attn_wide")) {  // channel-split attention (attn_cs_kernel): 0 off, 1 auto (C >= 384, S >= 256), 2 wherever it applies
+  if (!std::strcmp(key, "attn_wide")) {  // channel-split attention (attn_cs_kernel): 0 off, 1 auto (C >= 384 at S >= 256; C = 1024), 2 wherever it applies
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_wide in [0,2]");
     itsd::g_attn_wide = value;
     return ITSD_OK;

@@ -62,6 +62,10 @@ int main() {
   expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
   expect("set_option p4_w=16", itsd_set_option("p4_w", 16), ITSD_ERR_INVALID);
+  expect("set_option convt_prune=2", itsd_set_option("convt_prune", 2), ITSD_ERR_INVALID);
+  expect("set_option convt_prune=1 (default)", itsd_set_option("convt_prune", 1), ITSD_OK);
+  expect("set_option attn_wide=3", itsd_set_option("attn_wide", 3), ITSD_ERR_INVALID);
+  expect("set_option tail_px=96", itsd_set_option("tail_px", 96), ITSD_ERR_INVALID);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it
     std::string k(4096, 'k');
