@@ -1272,6 +1272,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_sub = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "small_minks")) {  // conv_small split K: at least this many 64-channel K-chunks a slice
+    if (value < 1 || value > 64) return fail(ITSD_ERR_INVALID, "small_minks in [1,64]");
+    itsd::g_small_minks = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "convt_prune")) {  // ConvTranspose2d sub-pixel phases skip their all-zero taps (p4 / conv_pipe)
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "convt_prune in [0,1]");
     itsd::g_convt_prune = value;

@@ -27,6 +27,7 @@ extern int g_small_8x8;      // conv_small (split K) for under-filled 8x8-level 
 extern int g_small_wide;     // conv_small for under-filled statistics-free convs of larger images ("small_wide")
 extern int g_attn_wide_nq;   // its query groups a block: 0 auto, 1 / 2 forced ("attn_wide_nq")
 extern int g_attn_wide;      // channel-split attention: 0 off, 1 auto, 2 wherever it applies ("attn_wide")
+extern int g_small_minks;  // conv_small split K: >= this many K-chunks a slice ("small_minks")
 extern int g_convt_prune;  // ConvTranspose2d sub-pixel phases skip their all-zero taps: 0 off, 1 on ("convt_prune")
 extern int g_subpix_split;  // under-filled sub-pixel conv_pipe launches split K in-launch: 0 off, 1 on ("subpix_split")
 extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")

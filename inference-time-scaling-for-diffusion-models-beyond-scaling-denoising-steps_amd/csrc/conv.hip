@@ -57,6 +57,8 @@ int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
+int g_small_minks = 8;    // conv_small split K: >= this many K-chunks a slice (itsd_set_option "small_minks"; 8 against
+                          // 2: N=32 step -2.3 %, N=64 -0.9 %, N=256 / C3 / C4 equal, profiles/r04/small_minks_ab.txt)
 int g_convt_prune = 1;    // ConvTranspose2d sub-pixel phases skip their all-zero taps (itsd_set_option "convt_prune")
 int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
@@ -3375,7 +3377,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
         (a.Hout * a.Wout <= 16 || wide || small8) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
       const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
-      S = std::min(std::min((512 + blocks - 1) / blocks, nK / 2), 16);  // <= 2 combine batches
+      S = std::min(std::min((512 + blocks - 1) / blocks, nK / g_small_minks), 16);  // <= 2 combine batches
       while (S > 1 && (long long)blocks * S * 4096 > a.splitk_cap) --S;
       if (S < 1) S = 1;
     }
