@@ -31,7 +31,9 @@ bool attn_flash_ok(int S, int C);
 bool attn_cs_ok(int S, int C);
 bool attn_block_ok(int S, int C);
 hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
-int g_attn_fuse = 1;  // fused AttnBlock kernel where it applies (itsd_set_option "attn_fuse", read at create)
+int g_attn_fuse = 2;  // fused AttnBlock kernel: 0 off, 1 at S = 64 and 16, 2 S = 64 only (shipped: the 4x4 middle
+                      // block fused -- 4 images a block -- measured 0.6 % slower at N = 32, equal at N = 256,
+                      // profiles/r04/attn_fuse_4x4_ab.txt) (itsd_set_option "attn_fuse", read at create)
 int g_tap_prune = 1;   // drop conv taps that read only padding for every output pixel ("tap_prune", read at create)
 int g_down_merge = 1;  // CFG DownSample c1 (3x3) + c2 (5x5) as one 5x5 conv ("down_merge", read at create)
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
@@ -528,7 +530,7 @@ struct Builder {
     if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
     if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
     else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
-    if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch)) {
+    if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch) && (H * W == 64 || itsd::g_attn_fuse == 1)) {
       // the whole AttnBlock in one launch (kernels.hip attn_block_kernel)
       const std::string a = p + ".attn";
       const int64_t cc = (int64_t)out_ch * out_ch;
@@ -964,6 +966,7 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
     a.out_stats = out.stats != SIZE_MAX ? (float*)(u->ws + out.stats) : nullptr;
     a.scale = (float)std::pow((double)o.C, -0.5);
     a.n = c.nb;
+    a.S = o.S;
     // attn_block_split_kernel's slabs in the split-K workspace (ops run in stream order; <= 4 MB of
     // partial scores at n * G <= 256, then the O slab)
     if ((long long)c.nb * 64 * o.C * 2 / 4 + (4ll << 20) / 4 <= itsd_unet::kSplitkCap) {
@@ -1330,8 +1333,9 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_attn_wide = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64); takes effect for UNets created afterwards
-    itsd::g_attn_fuse = value ? 1 : 0;
+  if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel: 0 off, 1 S = 64 and 16, 2 S = 64 only (UNets created afterwards)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_fuse in [0,2]");
+    itsd::g_attn_fuse = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "fuse_gn")) {  // takes effect for UNets created afterwards

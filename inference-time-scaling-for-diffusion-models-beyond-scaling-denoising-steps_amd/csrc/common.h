@@ -193,7 +193,7 @@ struct AttnArgs {
 
 // Fused AttnBlock at S = 64 (kernels.hip attn_block_kernel).
 struct AttnBlockArgs {
-  const bf16_t* x;        // [n][64][C] NHWC (the ResBlock output)
+  const bf16_t* x;        // [n][S][C] NHWC (the ResBlock output)
   const float* st;        // its GroupNorm statistics slab [n * spi][2][C]
   int spi;                // statistics slots per image
   const float* gamma; const float* beta;
@@ -201,10 +201,11 @@ struct AttnBlockArgs {
   const float* bqkv;      // [3C]
   const bf16_t* wp;       // [C/32][C/16][64][8]
   const float* bp;        // [C]
-  bf16_t* out;            // [n][64][C]
+  bf16_t* out;            // [n][S][C]
   float* out_stats;       // [n][2][C] (one slot per image) or null
   float scale;            // C^-0.5
   int n;
+  int S;                  // tokens an image: 64 (one image a block) or 16 (4 images a block)
   // attn_block_split_kernel (an image's work over G blocks, small batches): partial-score and O slabs
   // (write-through hand-offs) and two monotonic counters per image
   float* spart;           // [n][G][4 tiles][64 lanes][16] fp32

@@ -349,18 +349,22 @@ __device__ __forceinline__ void atl(int slot) {
 #define ATL(slot)
 #endif
 
-template <int C>
+template <int C, int IPB>
 __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
-  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
-  static_assert(C % 128 == 0, "C");
+  // IPB images of SI = 64 / IPB tokens a block (IPB = 4: the 4x4 middle block, S = 16), their 64 tokens
+  // projected together; the scores of a query are masked to its own image's keys
+  constexpr int S = 64, SI = S / IPB, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
+  static_assert(C % 128 == 0 && SI % 16 == 0, "C, SI");
   constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256, R_ST = R_GS + 32 * 2 * 4;
-  __shared__ __attribute__((aligned(16))) char sm[R_ST + 2 * C * 2 * 4];
+  // (IPB > 1: the group statistics of the images live in the V^T region until phase 1, and the
+  // consumer statistics go straight from the lanes to the slab: no R_GS / R_ST)
+  __shared__ __attribute__((aligned(16))) char sm[IPB == 1 ? R_ST + 2 * C * 2 * 4 : R_GS];
   const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wq = w & 3, wt = w >> 2;  // wave = (channel-block group, token block)
-  const int img = blockIdx.x;
+  const int img = blockIdx.x * IPB, nimg = min(IPB, a.n - img), ntok = nimg * SI;
   ATL(0);
-  const bf16_t* x = a.x + (size_t)img * S * C;
+  const bf16_t* x = a.x + (size_t)img * SI * C;
   // [row][C] bf16 image, 16-B chunk ch of row r at (ch ^ (r & 15))
   auto rowc = [](int r, int ch, int rowbytes) { return r * rowbytes + ((ch ^ (r & 15)) << 4); };
   // [row][64] bf16 image (128-B rows), chunk ch of row r at ch ^ ((r >> 1) & 7)
@@ -374,15 +378,18 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 #pragma unroll
   for (int i = 0; i < XU; ++i) {
     const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8);
-    xv[i] = *(const u32x4*)(x + (size_t)t * C + ch * 8);
+    xv[i] = t < ntok ? *(const u32x4*)(x + (size_t)t * C + ch * 8) : u32x4{0u, 0u, 0u, 0u};
   }
-  float* gs = (float*)(sm + R_GS);
-  if (tid < 256) {
-    const int g = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
+  float* gs = (float*)(sm + (IPB == 1 ? R_GS : R_VT));  // [image of the block][32 groups][mean, rstd]
+#pragma unroll
+  for (int p2 = 0; p2 < (IPB + 1) / 2; ++p2) {  // two images a pass (threads 0-255, 256-511)
+    const int il = 2 * p2 + (tid >> 8);
+    if (il >= nimg) continue;
+    const int g = (tid >> 3) & 31, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
     double s = 0.0, q = 0.0;
     for (int k = l8; k < n_it; k += 8) {
       const int c = g * gsz + k / a.spi;
-      const long long sl = (long long)img * a.spi + k % a.spi;
+      const long long sl = (long long)(img + il) * a.spi + k % a.spi;
       s += (double)a.st[(sl * 2) * C + c];
       q += (double)a.st[(sl * 2 + 1) * C + c];
     }
@@ -392,11 +399,11 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       q += __shfl_xor(q, o, 64);
     }
     if (l8 == 0) {
-      const double E = (double)gsz * S, mean = s / E;
+      const double E = (double)gsz * SI, mean = s / E;
       double var = q / E - mean * mean;
       var = var > 0.0 ? var : 0.0;
-      gs[2 * g] = (float)mean;
-      gs[2 * g + 1] = (float)(1.0 / sqrt(var + 1e-5));
+      gs[(il * 32 + g) * 2] = (float)mean;
+      gs[(il * 32 + g) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
     }
   }
   __syncthreads();
@@ -410,7 +417,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       float y[2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
-        const int c = c0 + 2 * e2 + h2, g = c / (C / 32);  // (an 8-channel chunk may straddle two groups)
+        const int c = c0 + 2 * e2 + h2, g = (IPB == 1 ? 0 : (t / SI) * 32) + c / (C / 32);  // (an 8-channel chunk may straddle two groups)
         const float mean = gs[2 * g], rstd = gs[2 * g + 1];
         const float sc = rstd * a.gamma[c];
         const float xf = __uint_as_float(h2 ? (xv[i][e2] & 0xffff0000u) : (xv[i][e2] << 16));
@@ -547,6 +554,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       v[e] = Sm[qry * (S + 4) + k0 + e];
+      if (IPB > 1 && (k0 + e) / SI != qry / SI) v[e] = -INFINITY;  // another image's key
       m = fmaxf(m, v[e]);
     }
 #pragma unroll
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
           if (w + 8 * b < CB) acc[tb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[tb][b], 0, 0, 0);
       }
     }
-    bf16_t* out = a.out + (size_t)img * S * C;
+    bf16_t* out = a.out + (size_t)img * SI * C;
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb) {
       const int tk = 32 * tb + rl;  // this lane's token
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * cb + 8 * g + 4 * hh;
           const f32x4 bb = *(const f32x4*)(a.bp + c);
-          const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
+          const uint2 rr = tk < ntok ? *(const uint2*)(x + (size_t)tk * C + c) : uint2{0u, 0u};
           const float v0 = acc[tb][b][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
           const float v1 = acc[tb][b][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
           const float v2 = acc[tb][b][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
@@ -663,7 +671,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
             o[d] = sw[0];
             o[2 + d] = sw[1];
           }
-          *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
+          if (tk < ntok) *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
         }
         if (a.out_stats) {  // this token block's 32 lanes: butterfly, then the two blocks summed in order
           auto xchg = [](float xf, auto wc) {
@@ -685,19 +693,45 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
               v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
             }
           };
-          halve(std::integral_constant<int, 16>{});
-          halve(std::integral_constant<int, 8>{});
-          halve(std::integral_constant<int, 4>{});
-          halve(std::integral_constant<int, 2>{});
-          halve(std::integral_constant<int, 1>{});
-          const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
-          spart[(tb * 2 + (rl >> 4)) * C + co] = v[0];
+          if constexpr (IPB == 1) {
+            halve(std::integral_constant<int, 16>{});
+            halve(std::integral_constant<int, 8>{});
+            halve(std::integral_constant<int, 4>{});
+            halve(std::integral_constant<int, 2>{});
+            halve(std::integral_constant<int, 1>{});
+            const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
+            spart[(tb * 2 + (rl >> 4)) * C + co] = v[0];
+          } else {
+            // 16-token images: the sums and the squares halved separately over the 16 lanes of an
+            // image (lane bits 0-3), so lane (image rl >> 4, e) ends with channel co's sum and square
+            // sum of its own image, stored straight to that image's slot
+            auto halve2 = [&](auto wc) {
+              constexpr int wd = decltype(wc)::value;
+              const bool up = (rl & wd) != 0;
+#pragma unroll
+              for (int hq = 0; hq < 2; ++hq)
+#pragma unroll
+                for (int ii = 0; ii < wd; ++ii) {
+                  const float lo = v[16 * hq + ii], hi = v[16 * hq + ii + wd];
+                  v[16 * hq + ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+                }
+            };
+            halve2(std::integral_constant<int, 8>{});
+            halve2(std::integral_constant<int, 4>{});
+            halve2(std::integral_constant<int, 2>{});
+            halve2(std::integral_constant<int, 1>{});
+            const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3), il = tk / SI;
+            if (il < nimg) {
+              a.out_stats[(long long)(img + il) * 2 * C + co] = v[0];
+              a.out_stats[(long long)(img + il) * 2 * C + C + co] = v[16];
+            }
+          }
         }
       }
     }
   }
   ATL(6);  // proj + epilogue (wave's own)
-  if (a.out_stats) {
+  if (IPB == 1 && a.out_stats) {
     __syncthreads();
     for (int i = tid; i < 2 * C; i += 512)  // (sum | sum of squares) x channel: token block 0 + block 1
       a.out_stats[(long long)img * 2 * C + i] = spart[i] + spart[2 * C + i];
@@ -1088,20 +1122,32 @@ int attn_split_g(int n, int C) {
 }
 
 hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
-  if (a.spart && a.oslab && a.sync) {
+  if (a.spart && a.oslab && a.sync && a.S == 64) {
     const int G = attn_split_g(a.n, C);
     if (G == 6) ITSD_LAUNCH((attn_block_split_kernel<384, 6>), dim3(a.n * 6), dim3(512), 0, s, a);
     else if (G == 4) ITSD_LAUNCH((attn_block_split_kernel<384, 4>), dim3(a.n * 4), dim3(512), 0, s, a);
     else if (G == 2) ITSD_LAUNCH((attn_block_split_kernel<384, 2>), dim3(a.n * 2), dim3(512), 0, s, a);
     if (G) return hipGetLastError();
   }
-  if (C == 384) ITSD_LAUNCH(attn_block_kernel<384>, dim3(a.n), dim3(512), 0, s, a);
-  else if (C == 256) ITSD_LAUNCH(attn_block_kernel<256>, dim3(a.n), dim3(512), 0, s, a);
-  else if (C == 128) ITSD_LAUNCH(attn_block_kernel<128>, dim3(a.n), dim3(512), 0, s, a);
+  if (a.S == 16) {  // 4 images a block
+    const dim3 g4((unsigned)((a.n + 3) / 4));
+    if (C == 512) ITSD_LAUNCH((attn_block_kernel<512, 4>), g4, dim3(512), 0, s, a);
+    else if (C == 384) ITSD_LAUNCH((attn_block_kernel<384, 4>), g4, dim3(512), 0, s, a);
+    else if (C == 256) ITSD_LAUNCH((attn_block_kernel<256, 4>), g4, dim3(512), 0, s, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (a.S != 64) return hipErrorInvalidValue;
+  if (C == 384) ITSD_LAUNCH((attn_block_kernel<384, 1>), dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 256) ITSD_LAUNCH((attn_block_kernel<256, 1>), dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 128) ITSD_LAUNCH((attn_block_kernel<128, 1>), dim3(a.n), dim3(512), 0, s, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
-bool attn_block_ok(int S, int C) { return S == 64 && (C == 128 || C == 256 || C == 384); }  // LDS: C <= 384
+// S = 64: one image a block (LDS: C <= 384); S = 16 (the 4x4 middle block): 4 images a block, C <= 512
+bool attn_block_ok(int S, int C) {
+  return (S == 64 && (C == 128 || C == 256 || C == 384)) || (S == 16 && (C == 256 || C == 384 || C == 512));
+}
 
 // Flash-style MFMA attention for long sequences (S > 256: the CFG UNet's 32x32 level,
 // S = 1024, C = 128, ModelCondition.py:98-118; Arch A at 64/256 px). No S x S tile is

@@ -67,6 +67,8 @@ int main() {
   expect("set_option attn_wide=3", itsd_set_option("attn_wide", 3), ITSD_ERR_INVALID);
   expect("set_option tail_px=96", itsd_set_option("tail_px", 96), ITSD_ERR_INVALID);
   expect("set_option small_minks=0", itsd_set_option("small_minks", 0), ITSD_ERR_INVALID);
+  expect("set_option attn_fuse=3", itsd_set_option("attn_fuse", 3), ITSD_ERR_INVALID);
+  expect("set_option attn_fuse=2 (default)", itsd_set_option("attn_fuse", 2), ITSD_OK);
   expect("set_option small_minks=8 (default)", itsd_set_option("small_minks", 8), ITSD_OK);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it

@@ -1,5 +1,6 @@
 """attn_block_kernel: the whole AttnBlock (Model.py:145-164: GroupNorm, q|k|v 1x1, softmax(q k^T /
-sqrt(C)) v, proj 1x1, residual) of Arch A's 8x8 level in one launch, against the unfused path
+sqrt(C)) v, proj 1x1, residual) of Arch A's 8x8 level (one image a block) and of its 4x4 middle block
+(4 images of 16 tokens a block, scores masked to the query's image) in one launch, against the unfused path
 (gn_apply + q|k|v conv + attn_mfma_kernel + proj conv, attn_fuse=0 at create) and the oracle.
 Both paths round hn, q / k / v, P and O to bf16; the sums run in other orders, so they agree
 within 1.5e-2 relative L2 (bf16 tolerance) rather than bit for bit."""
@@ -19,22 +20,27 @@ def _rel_l2(a, b):
     return (torch.linalg.norm((a - b).flatten()) / torch.linalg.norm(b.flatten())).item()
 
 
-def _net(fuse):
+ATTN_FUSE_DEFAULT = 2  # shipped: fused at S = 64 only (the 4x4 middle block fused, attn_fuse = 1, measured slower at N = 32)
+
+
+def _net(fuse, n=8):
+    """A UNet whose native handle (capacity >= n, so no later re-create with other options) is built
+    under attn_fuse = fuse."""
     a = ARCH_A
     rt.set_option("attn_fuse", fuse)
     try:
         net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision="bf16")
         net.load_state_dict(synthetic_state_dict(a, 0))
         net.to("cuda:0")
-        net.native(8)  # the handle is built (and the option read) here
+        net.native(max(n, 8))  # the handle is built (and the option read) here
     finally:
-        rt.set_option("attn_fuse", 1)
+        rt.set_option("attn_fuse", ATTN_FUSE_DEFAULT)
     return net
 
 
-@pytest.mark.parametrize("n", [8, 256])
+@pytest.mark.parametrize("n", [8, 256, 6, 13])  # (6, 13: a last 4x4 block with 2 / 1 images)
 def test_fused_attnblock_vs_unfused_and_oracle(n):
-    fused, plain = _net(1), _net(0)
+    fused, plain = _net(1, n), _net(0, n)
     gen = torch.Generator().manual_seed(900 + n)
     x = torch.randn(n, 3, 32, 32, generator=gen)
     t = torch.randint(0, 1000, (n,), generator=gen)
@@ -51,9 +57,26 @@ def test_fused_attnblock_vs_unfused_and_oracle(n):
     assert d < 1.5e-2 and _rel_l2(ef[idx], ref) < 2e-2
 
 
+def test_fused_attnblock_4x4_vs_8x8_only():
+    """The 4x4 middle block fused (attn_fuse = 1, shipped) against fused at 8x8 only (attn_fuse = 2: the
+    middle block on gn_apply + q|k|v conv + attn_mfma_kernel + proj conv): within bf16 tolerance."""
+    n = 12
+    only8, both = _net(2, n), _net(1, n)
+    gen = torch.Generator().manual_seed(950)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, 1000, (n,), generator=gen)
+    for net, fused in ((both, True), (only8, False)):  # the two handles run different 4x4 kernels
+        k4 = [o["kernel"] for o in net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda()) if o["H"] == 4]
+        assert any("attn_block_kernel<512, 4>" in k for k in k4) == fused, k4
+    # (same roundings -- hn, q / k / v, P, O in bf16 -- and the same k order: measured bit-identical)
+    d = _rel_l2(both(x.cuda(), t.cuda()).float().cpu(), only8(x.cuda(), t.cuda()).float().cpu())
+    print(f"n={n}: 4x4 AttnBlock fused vs unfused rel-L2 {d:.2e}")
+    assert d < 1e-2
+
+
 def test_fused_attnblock_census():
-    net = _net(1)
     n = 16
+    net = _net(1, n)
     x = torch.randn(n, 3, 32, 32, device="cuda")
     t = torch.full((n,), 500, dtype=torch.int32, device="cuda")
     ops = net.native(n).profile_ops(x, t)
@@ -63,6 +86,9 @@ def test_fused_attnblock_census():
     assert all("attn_block_" in o["kernel"] for o in at8 if o["kind"] == "attnblock")
     # n = 16: the image's work spread over 6 blocks (16 x 6 <= 256 CUs)
     assert all("attn_block_split_kernel<384, 6>" in o["kernel"] for o in at8 if o["kind"] == "attnblock"), at8
+    # the 4x4 middle block (S = 16, C = 512): one launch, 4 images a block
+    at4 = [o for o in ops if o["H"] == 4 and o["kind"] in ("attnblock", "attn", "gn")]
+    assert [o["kind"] for o in at4] == ["attnblock"] and "attn_block_kernel<512, 4>" in at4[0]["kernel"], at4
 
 
 def _eps_with_split(net, x, t, split):
@@ -79,7 +105,7 @@ def test_split_attnblock_vs_single_block_and_oracle(n):
     hand-offs; auto G at n = 8 / 32: 6, 64: 4, 128: 2) against attn_block_kernel (one block per image,
     attn_split = 0) and the oracle. Only the score sum runs in another order (G partial sums): within
     bf16 tolerance of the single-block kernel, deterministic run to run; forced G = 2 / 4 / 6 at n = 8."""
-    net = _net(1)
+    net = _net(ATTN_FUSE_DEFAULT, n)
     gen = torch.Generator().manual_seed(1300 + n)
     x = torch.randn(n, 3, 32, 32, generator=gen)
     t = torch.randint(0, 1000, (n,), generator=gen)
