@@ -354,20 +354,25 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
         a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
       }
     } else {
-      for (int item = tid; item < S * BM; item += NT) {
-        const int s = item / BM, cl = item % BM;
+      // items (slot, 4 consecutive couts): 16-B column reads of E and 16-B stores of the 4 sums and the
+      // 4 square sums (the per-channel arithmetic of one item per cout; host: Cout % 4 == 0)
+      for (int item = tid; item < S * (BM / 4); item += NT) {
+        const int s = item / (BM / 4), cl = (item % (BM / 4)) * 4;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
-        float sum = 0.f, sq = 0.f;
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
         for (int k = 0; k < Gt; ++k) {
-          const float v = E[(s * Gt + k) * ER + cl];
-          sum += v;
-          sq = fmaf(v, v, sq);
+          const f32x4 v = *(const f32x4*)(E + (s * Gt + k) * ER + cl);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sum[e] += v[e];
+            sq[e] = fmaf(v[e], v[e], sq[e]);
+          }
         }
         const int spp = HWo >= 128 ? HWo / 128 : 1;
         const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * spp + phase * spp + (p0 % HWo) / Gt;
-        a.stats[(slot * 2) * a.Cout + co] = sum;
-        a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
+        *(f32x4*)(a.stats + (slot * 2) * a.Cout + co) = sum;
+        *(f32x4*)(a.stats + (slot * 2 + 1) * a.Cout + co) = sq;
       }
     }
   }

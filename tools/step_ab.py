@@ -33,7 +33,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="base")
     ap.add_argument("--create-set", default="", help="options set before the UNet is created, e.g. attn_fuse=2")
+    ap.add_argument("--lib", default="", help="another build of libitsd_hip.so (A/B of two builds in two processes)")
     args = ap.parse_args()
+    if args.lib:
+        rt.LIB_PATH = os.path.abspath(args.lib)
     for kv in filter(None, args.create_set.split("+")):
         k, val = kv.split("=")
         rt.set_option(k, int(val))
