@@ -336,22 +336,23 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
         *(f32x4*)(R + (pg * 2 + 1) * BM + 4 * cq) = q4;
       }
       __syncthreads();
-      // pass 2: groups -> slots in fixed order (deterministic)
+      // pass 2: groups -> slots in fixed order (deterministic); an item = 4 consecutive couts of a slot
+      // (16-B reads and stores, the per-channel sums unchanged; host: Cout % 4 == 0)
       const int gps = Gt / 16;
-      for (int item = tid; item < S * BM; item += NT) {
-        const int s = item / BM, cl = item % BM;
+      for (int item = tid; item < S * (BM / 4); item += NT) {
+        const int s = item / (BM / 4), cl = (item % (BM / 4)) * 4;
         const int co = tileC + cl, p0 = tileP + s * Gt;
         if (co >= a.Cout || p0 >= a.M) continue;
-        float sum = 0.f, sq = 0.f;
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f}, sq = {0.f, 0.f, 0.f, 0.f};
         for (int g = s * gps; g < (s + 1) * gps; ++g) {
-          sum += R[(g * 2) * BM + cl];
-          sq += R[(g * 2 + 1) * BM + cl];
+          sum += *(const f32x4*)(R + (g * 2) * BM + cl);
+          sq += *(const f32x4*)(R + (g * 2 + 1) * BM + cl);
         }
         // sub-pixel phases: spp slots per phase image (one when the phase image is below a slot)
         const int spp = HWo >= 128 ? HWo / 128 : 1;
         const long long slot = phase < 0 ? p0 / Gt : (long long)(p0 / HWo) * 4 * spp + phase * spp + (p0 % HWo) / Gt;
-        a.stats[(slot * 2) * a.Cout + co] = sum;
-        a.stats[(slot * 2 + 1) * a.Cout + co] = sq;
+        *(f32x4*)(a.stats + (slot * 2) * a.Cout + co) = sum;
+        *(f32x4*)(a.stats + (slot * 2 + 1) * a.Cout + co) = sq;
       }
     } else {
       // items (slot, 4 consecutive couts): 16-B column reads of E and 16-B stores of the 4 sums and the
