@@ -136,14 +136,25 @@ def census(net, n: int, img: int, labels=None):
 
 
 def conv_alg_bytes(o) -> float:
-    """Algorithmic HBM bytes of one bf16 conv launch: input activations once, weights once,
-    output once (the GroupNorm statistics and bias rows are negligible)."""
+    """Algorithmic HBM bytes of one bf16 conv launch, every operand once: input activations, weights,
+    output, the residual operand when the op adds one (ResBlock block2 / shortcut sums, Model.py:184),
+    the output's GroupNorm statistics slab (fp32 sum and square sum per channel and slot of
+    min(HW, 128) pixels) and, for a fused GroupNorm+SiLU input, the input's statistics slab read."""
     ks = max(1, o["ks"])
     cin = o["K"] // (ks * ks)
     su = o["stride_up"]
     stride, ups = su // 10, su % 10
     m_in = o["M"] * stride * stride if not ups else o["M"] // 4
-    return 2.0 * (m_in * cin + o["N"] * o["K"] + o["M"] * o["N"])
+    b = 2.0 * (m_in * cin + o["N"] * o["K"] + o["M"] * o["N"])
+    if o.get("resid"):
+        b += 2.0 * o["M"] * o["N"]
+    hw_out = o["H"] * o["H"]
+    if o.get("stats_out"):
+        b += 4.0 * 2 * (o["M"] / min(hw_out, 128)) * o["N"]
+    if o.get("gn_in"):
+        hw_in = hw_out * stride * stride if not ups else hw_out // 4
+        b += 4.0 * 2 * (m_in / min(hw_in, 128)) * cin
+    return b
 
 
 def rocprof_name(kernel: str) -> str:
@@ -227,7 +238,8 @@ def dominant_roofline(ops, agg, nat, x, t, precision: str, steady: bool = True):
         ims = sum(ms_of[i] for i in ii)
         ifl = sum(ops[i]["flops"] for i in ii)
         insts.append({"kernel": rocprof_name(name), "launches_per_forward": len(ii),
-                      "avg_launch_ms": round(ims / len(ii), 4), "tflops": round(ifl / (ims * 1e-3) / 1e12, 2)})
+                      "avg_launch_ms": round(ims / len(ii), 4), "tflops": round(ifl / (ims * 1e-3) / 1e12, 2),
+                      "alg_bytes": round(sum(conv_alg_bytes(ops[i]) for i in ii) / len(ii))})
     return func, {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                   "frac": round(achieved / peak, 4), "kernel": func,
                   "family": KERNEL_NAMES[kind], "launches_per_forward": n_l,
@@ -406,6 +418,7 @@ def main():
             tot_n = sum(ins["launches_per_forward"] for ins in roof["instantiations"])
             for ins in roof["instantiations"]:
                 ins["traffic"] = live[ins["kernel"]]
+                ins["traffic_ratio"] = round(ins["traffic"] / ins["alg_bytes"], 3)  # PMC / algorithmic bytes
             traffic = tot_b / tot_n
             tfiles = "live: rocprofv3 --pmc FETCH_SIZE (x2) + WRITE_SIZE in this run"
         elif args.precision == "bf16" and n_local == 256:
@@ -418,6 +431,7 @@ def main():
                 with open(tfile) as fh:
                     tb = json.load(fh).get("hbm_bytes_per_launch")
                 ins["traffic"] = tb
+                ins["traffic_ratio"] = round(tb / ins["alg_bytes"], 3)
                 tot_b += tb * ins["launches_per_forward"]
                 tot_n += ins["launches_per_forward"]
                 tfiles.append(os.path.relpath(tfile, ROOT))
@@ -426,6 +440,24 @@ def main():
         dom = [o for o in ops if o["kind"] in CONV_KINDS and kernel_function(o["kernel"] or o["kind"]) == kernel]
         alg_b = sum(conv_alg_bytes(o) for o in dom) / len(dom)
         avg_s = roof["avg_launch_ms"] * 1e-3
+        # on-box calibration ("re-measure both on the box"): the achievable bf16 MFMA rate
+        # (random operands, every CU) and HBM streaming rate of THIS device, and the fractions against
+        # them, so that a round-to-round delta can be told from the +-5-8 % spread between boxes
+        calib = None
+        try:
+            from itsd import runtime as rt
+            progress("calibration: bf16 MFMA loop, HBM copy")
+            mf, hb = rt.calibrate(rt.CALIB_MFMA_BF16), rt.calibrate(rt.CALIB_HBM_COPY)
+            calib = {"mfma_bf16_tflops": round(mf, 1), "hbm_copy_gbps": round(hb, 1),
+                     "mfma_frac_of_spec": round(mf / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "hbm_frac_of_spec": round(hb / HBM_PEAK_GBPS, 4),
+                     "method": "v_mfma_f32_32x32x16_bf16 chains on random operands, 2 waves/SIMD on every CU; "
+                               "1 GiB 16-B/lane copy (read + write bytes); best of 3 after a warm launch"}
+            if args.precision == "bf16":
+                calib["dominant_frac_of_measured"] = round(roof["achieved"] / mf, 4)
+        except Exception as e:  # the line stands without it
+            calib = {"error": repr(e)}
+        roof["calibration"] = calib
         roof.update({
             "traffic": traffic,
             "traffic_source": tfiles if traffic is not None else None,
@@ -439,6 +471,9 @@ def main():
                          "pmc_bytes_per_launch": traffic,
                          "pmc_gbps": round(traffic / avg_s / 1e9, 1) if traffic else None,
                          "pmc_frac_of_peak": round(traffic / avg_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
+                         "pmc_frac_of_measured": (round(traffic / avg_s / 1e9 / calib["hbm_copy_gbps"], 4)
+                                                  if traffic and calib and calib.get("hbm_copy_gbps") else None),
+                         "traffic_ratio": round(traffic / alg_b, 3) if traffic else None,
                          "peak_gbps": HBM_PEAK_GBPS},
         })
         # attention (north_star: MFMA utilisation): the fused AttnBlock kernel (GroupNorm, q|k|v and

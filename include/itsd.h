@@ -55,6 +55,9 @@ extern "C" {
 #define ITSD_ERR_WEIGHTS 3   /* state_dict key or shape mismatch (load_state_dict strict) */
 #define ITSD_ERR_NAN 4       /* the sampler produced a NaN (Diffusion.py:100 assert) */
 #define ITSD_ERR_OOM 5
+#define ITSD_ERR_HANDOFF 6   /* an in-kernel cross-block hand-off wait exhausted its poll bound (the grid was not
+                                co-resident); its outputs are NaN. Reported by itsd_sampler_run with ITSD_RUN_SYNC
+                                and by itsd_unet_query(u, "status", ...) after itsd_unet_forward */
 
 enum { ITSD_ARCH_DDPM = 0, ITSD_ARCH_CFG = 1 };
 enum { ITSD_PREC_FP32 = 0, ITSD_PREC_BF16 = 1 };
@@ -141,7 +144,8 @@ int itsd_verify_paired(const float* images, const float* ref_features, int n_can
  * qkv: [n][S][3C] (q | k | v per token, the fused projection the UNet produces);
  * precision ITSD_PREC_FP32: fp32 tensors; ITSD_PREC_BF16: bf16 tensors and vt, the
  * channel-major V [n][C][S] (the MFMA kernels read V^T; S <= 256: whole-row kernel,
- * S > 256: flash kernel, C in {64,128,256}), out [n][S][C]. */
+ * S > 256: the flash kernel, S % 32 == 0 and C in {64,128,256}, or the channel-split kernel,
+ * S % 64 == 0 and C in {256,384,512,1024}), out [n][S][C]. */
 int itsd_attention(const void* qkv, const void* vt, void* out, int n, int S, int C, int precision, void* stream);
 
 /* Census of one forward at batch n (synchronous): runs the op program eagerly with
@@ -156,10 +160,11 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
  * kind the op class (0 GN, 1 conv, 2 attention, 3 GN finalize, 4/5/6 fused GroupNorm conv
  * 128 px / 256 px / 8x8 level; -1 head, -2 tail, as a signed byte) and kernel the id of
  * the first kernel the launch ran (itsd_kernel_name), ms[i], flops[i] and shapes[8*i..] =
- * {M, Cout, K or Cin, Hout, ksize, 10*stride+upsample, op, 0} with op the program op index
+ * {M, Cout, K or Cin, Hout, ksize, 10*stride+upsample, op, flags} with op the program op index
  * (1-based, itsd_profile_op's numbering; 0 = head / tail). Ops whose launch is folded into the
  * next one (a GroupNorm finalize done by conv3x3_gn_p5_kernel) have no entry. kind 7 = the fused
- * AttnBlock. CFG UNets run with label 0.
+ * AttnBlock. flags: bit 0 the op adds a residual, bit 1 it writes its output's GroupNorm statistics, bit 2
+ * its input GroupNorm(+SiLU) is fused (statistics read). CFG UNets run with label 0.
  * At most max_ops entries; *n_ops = entries written. */
 int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int max_ops, int* kinds,
                      double* ms, double* flops, int* shapes, int* n_ops, void* stream);
@@ -182,12 +187,22 @@ int itsd_set_option(const char* key, int value);
 
 /* Introspection of a handle (no device work): "graph_captures" (step graphs captured and
  * instantiated so far; a search replays one graph across all its rounds), "max_batch",
- * "T_sched", "ws_bytes" (activation arena), "ops" (program length). */
+ * "T_sched", "ws_bytes" (activation arena), "ops" (program length); and, synchronising the
+ * handle's stream, "status" = the in-kernel hand-off status word of the last forward / sampler run
+ * (0 ok; bit 0: attn_block_split_kernel's wait exhausted its bound -- ITSD_ERR_HANDOFF). */
 int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value);
 
 /* Name of census kernel id `id` (itsd_profile_ops): the launch site's kernel expression,
  * e.g. "conv3x3_gn_p4_kernel<32>"; "" for 0 / unknown ids. */
 const char* itsd_kernel_name(int id);
+
+/* On-box peak calibration (synchronous on stream; measurement only, no reference counterpart):
+ * ITSD_CALIB_MFMA_BF16 -> *value = the achievable dense bf16 MFMA rate in TFLOP/s (v_mfma_f32_32x32x16_bf16
+ * chains on random operands, every CU, 2 waves per SIMD); ITSD_CALIB_HBM_COPY -> *value = the achievable
+ * HBM streaming rate in GB/s (a 1 GiB 16-B-per-lane copy, bytes read + written). bench.py reports its
+ * roofline fractions against these as well as against the datasheet peaks. */
+enum { ITSD_CALIB_MFMA_BF16 = 0, ITSD_CALIB_HBM_COPY = 1 };
+int itsd_calibrate(int what, double* value, void* stream);
 
 const char* itsd_last_error(void);
 int itsd_version(void);

@@ -31,9 +31,7 @@ bool attn_flash_ok(int S, int C);
 bool attn_cs_ok(int S, int C);
 bool attn_block_ok(int S, int C);
 hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
-int g_attn_fuse = 2;  // fused AttnBlock kernel: 0 off, 1 at S = 64 and 16, 2 S = 64 only (shipped: the 4x4 middle
-                      // block fused -- 4 images a block -- measured 0.6 % slower at N = 32, equal at N = 256,
-                      // profiles/r04/attn_fuse_4x4_ab.txt) (itsd_set_option "attn_fuse", read at create)
+int g_attn_fuse = 1;  // fused AttnBlock kernel at S = 64 (Arch A's 8x8 level): 0 off, 1 on (itsd_set_option "attn_fuse", read at create)
 int g_tap_prune = 1;   // drop conv taps that read only padding for every output pixel ("tap_prune", read at create)
 int g_down_merge = 1;  // CFG DownSample c1 (3x3) + c2 (5x5) as one 5x5 conv ("down_merge", read at create)
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
@@ -43,6 +41,7 @@ hipError_t launch_linear(const float*, int, int, const float*, const float*, int
 hipError_t launch_verify(int, const float*, int, int, int, int, int, double*, const float*, hipStream_t);
 hipError_t launch_set_int(int*, int, hipStream_t);
 hipError_t launch_add_int(int*, int, hipStream_t);
+int calibrate_run(int what, double* value, hipStream_t s);
 hipError_t launch_run_begin(int*, int, int*, RunParams*, const RunParams&, hipStream_t);
 int g_option_gen = 0;  // bumped by every itsd_set_option: part of the step-graph cache key
 bool conv_gn_eligible(int H, int W);
@@ -83,6 +82,13 @@ int fail(int code, const std::string& msg) {
     if (r_ != ITSD_OK) return r_; \
   } while (0)
 
+// ITSD_ERR_HANDOFF's message from the status word's bits (AttnBlockArgs::err)
+std::string handoff_msg(int bits) {
+  std::string m = "in-kernel hand-off wait exhausted its poll bound (grid not co-resident?):";
+  if (bits & 1) m += " attn_block_split_kernel";
+  return m;
+}
+
 uint16_t host_f2bf(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -116,7 +122,6 @@ struct Op {
   int subpix = 0;  // upsample conv as 4 phase-wise 2x2 convs (conv.hip conv_pipe)
   size_t wt = 0, bias = 0;
   size_t wfrag = SIZE_MAX;  // fragment-ordered copy of wt (fused GroupNorm convs: conv3x3_gn_p4 / p5_kernel)
-  size_t wfrag16 = SIZE_MAX;  // the same for the 16x16x32 MFMA (conv3x3_gn_p4_kernel<.., true>)
   int Cout = 0, K = 0;
   int temb_col = -1;
   int resid = -1;
@@ -279,22 +284,6 @@ struct Builder {
   }
   // [Cout][K] bf16 (k = (ky*ks+kx)*Cin + ci) -> MFMA A-fragment order [Cout/32][K/16][64][8]:
   // lane L of k-step s holds W[32*cb + (L & 31)][16*s + 8*(L >> 5) + e] (v_mfma_f32_32x32x16_bf16).
-  // A fragments of v_mfma_f32_16x16x32_bf16: lane L holds cout 16 cb + L % 16, k = 32 st + 8 (L / 16) + e
-  size_t pack_frag16(const float* Wsrc, int Cout, int Cin, int ks) {
-    const int K = ks * ks * Cin, nks = K / 32;
-    std::vector<uint16_t> b((size_t)Cout * K, 0);
-    if (Wsrc)
-      for (int cb = 0; cb < Cout / 16; ++cb)
-        for (int st = 0; st < nks; ++st)
-          for (int L = 0; L < 64; ++L)
-            for (int e = 0; e < 8; ++e) {
-              const int co = 16 * cb + (L & 15), k = 32 * st + 8 * (L >> 4) + e;
-              const int tap = k / Cin, ci = k - tap * Cin, ky = tap / ks, kx = tap - ky * ks;
-              b[(((size_t)cb * nks + st) * 64 + L) * 8 + e] =
-                  host_f2bf(Wsrc[(((size_t)co * Cin + ci) * ks + ky) * ks + kx]);
-            }
-    return ar.add(b.data(), b.size() * 2);
-  }
   size_t pack_frag(const float* Wsrc, int Cout, int Cin, int ks) {
     const int K = ks * ks * Cin, nks = K / 16;
     std::vector<uint16_t> b((size_t)Cout * K, 0);
@@ -494,8 +483,6 @@ struct Builder {
                         Cin % 128 == 0 && Hout == Wout && (Hout == 32 || Hout == 16 || Hout == 8);
     if ((coef != SIZE_MAX || plain3) && u->bf16 && Cout % 32 == 0 && (ks * ks * Cin) % 16 == 0)
       u->ops.back().wfrag = pack_frag(W, Cout, Cin, ks);
-    if (coef != SIZE_MAX && u->bf16 && Cout % 16 == 0 && (ks * ks * Cin) % 32 == 0 && ks == 3 && Hout >= 16)
-      u->ops.back().wfrag16 = pack_frag16(W, Cout, Cin, ks);
     return dst;
   }
   // conv3x3(silu(GroupNorm(s1 ++ s2))) can run as one fused launch (conv3x3_gn_kernel)
@@ -530,7 +517,7 @@ struct Builder {
     if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
     if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
     else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
-    if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch) && (H * W == 64 || itsd::g_attn_fuse == 1)) {
+    if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch)) {
       // the whole AttnBlock in one launch (kernels.hip attn_block_kernel)
       const std::string a = p + ".attn";
       const int64_t cc = (int64_t)out_ch * out_ch;
@@ -846,7 +833,6 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     a.ksize = o.ksize; a.stride = o.stride; a.pad = o.pad; a.upsample = o.upsample;
     a.wt = u->wdev + o.wt;
     a.wfrag = o.wfrag != SIZE_MAX ? u->wdev + o.wfrag : nullptr;
-    a.wfrag16 = o.wfrag16 != SIZE_MAX ? u->wdev + o.wfrag16 : nullptr;
     a.Cout = o.Cout; a.K = o.K;
     a.bias = u->wp(o.bias);
     if (o.temb_col >= 0) {
@@ -877,6 +863,7 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     }
     a.zins = o.zins;
     a.dbg = itsd::g_conv_dbg;
+    a.xcd = itsd::g_p4_xcd;
     if (o.subpix) {  // input-grid GEMM with 2x2 (upsample) / 3x3 (ConvTranspose2d) taps per phase (conv.hip)
       a.subpix = o.subpix;
       a.Hout = in.H; a.Wout = in.W;
@@ -974,6 +961,8 @@ int launch_op(itsd_unet* u, const Op& o, const RunCtx& c, hipStream_t s) {
       a.oslab = (bf16_t*)(u->splitk_ws + (4ll << 20) / 4);
       a.sync = u->attn_sync;
     }
+    a.err = u->d_nan + 1;
+    a.spin_bound = itsd::g_spin_bound;
     e = launch_attn_block(a, o.C, s);
   } else {
     AttnArgs a{};
@@ -1171,8 +1160,8 @@ const char* itsd_kernel_name(int id) {
 int itsd_set_option(const char* key, int value) {
   if (!key) return fail(ITSD_ERR_INVALID, "null key");
   ++itsd::g_option_gen;  // cached step graphs baked in the previous kernel choices
-  if (!std::strcmp(key, "conv_variant")) {
-    if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "conv_variant in [0,3]");
+  if (!std::strcmp(key, "conv_variant")) {  // 2: conv_pipe (shipped); 1: conv_igemm (register-staged, parity checks)
+    if (value < 1 || value > 2) return fail(ITSD_ERR_INVALID, "conv_variant in [1,2]");
     itsd::g_conv_variant = value;
     return ITSD_OK;
   }
@@ -1188,11 +1177,6 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "conv1x1")) {  // streaming 1x1 conv kernel for statistics-free 1x1 convs of large pixel counts
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "conv1x1 in [0,2]");
     itsd::g_conv1x1 = value;
-    return ITSD_OK;
-  }
-  if (!std::strcmp(key, "tail_px")) {  // tail_mfma_kernel output pixels a block
-    if (value != 64 && value != 128) return fail(ITSD_ERR_INVALID, "tail_px in {64, 128}");
-    itsd::g_tail_px = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "small_8x8")) {  // conv_small (split K) for under-filled 8x8-level convs
@@ -1232,20 +1216,6 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_gn_wide = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "conv_wide")) {  // round 3's 256-pixel plain conv (deleted): only 0 is accepted
-    if (value != 0) return fail(ITSD_ERR_INVALID, "conv_wide: the 256-pixel plain conv was removed (only 0)");
-    itsd::g_conv_wide = 0;
-    return ITSD_OK;
-  }
-  if (!std::strcmp(key, "gn_reg")) {  // 4: conv3x3_gn_p4_kernel; the superseded generations 0-3 were removed
-    if (value != 4) return fail(ITSD_ERR_INVALID, "gn_reg: only 4 (conv3x3_gn_p4_kernel) exists");
-    itsd::g_gn_reg = value;
-    return ITSD_OK;
-  }
-  if (!std::strcmp(key, "small_korder")) {  // conv_small K order: 1 taps inside each channel chunk, 0 tap-major
-    itsd::g_small_korder = value ? 1 : 0;
-    return ITSD_OK;
-  }
   if (!std::strcmp(key, "attn_cs")) {  // attn_mfma_kernel output-channel slices: 0 auto, 1..8 forced
     if (value < 0 || value > 8) return fail(ITSD_ERR_INVALID, "attn_cs in [0,8]");
     itsd::g_attn_cs = value;
@@ -1256,18 +1226,24 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_attn_aq = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "p4_m16")) {  // conv3x3_gn_p4_kernel at W = 32 / 16 on v_mfma_f32_16x16x32_bf16
-    itsd::g_p4_m16 = value ? 1 : 0;
-    return ITSD_OK;
-  }
-  if (!std::strcmp(key, "p4_w")) {  // levels conv3x3_gn_p4_kernel takes (bit 0 W = 8, 1 W = 16, 2 W = 32, 3 W = 64); others p5 / 128-px
-    if (value < 0 || value > 15) return fail(ITSD_ERR_INVALID, "p4_w in [0,15]");
+  if (!std::strcmp(key, "p4_w")) {  // levels conv3x3_gn_p4_kernel takes (bit 0 W = 8, 1 W = 16, 2 W = 32); others p5 / 128-px
+    if (value < 0 || value > 7) return fail(ITSD_ERR_INVALID, "p4_w in [0,7]");
     itsd::g_p4_w = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "splitk_inl")) {  // conv_pipe split-K: 1 in-launch ticket combine, 0 splitk_epilogue_kernel
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "splitk_inl in [0,1]");
     itsd::g_splitk_inl = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "spin_bound")) {  // diagnostic: polls before an in-kernel hand-off wait fails (shipped 1 << 22)
+    if (value < 0) return fail(ITSD_ERR_INVALID, "spin_bound >= 0");
+    itsd::g_spin_bound = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p4_xcd")) {  // conv3x3_gn_p4_kernel: deal each XCD a contiguous range of tiles (0 off, 1 on)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_xcd in [0,1]");
+    itsd::g_p4_xcd = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p4_sub")) {  // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form: 0 off, 1 on
@@ -1333,8 +1309,8 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_attn_wide = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel: 0 off, 1 S = 64 and 16, 2 S = 64 only (UNets created afterwards)
-    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_fuse in [0,2]");
+  if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64): 0 off, 1 on (UNets created afterwards)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "attn_fuse in [0,1] (the 16-token form was removed)");
     itsd::g_attn_fuse = value;
     return ITSD_OK;
   }
@@ -1347,6 +1323,15 @@ int itsd_set_option(const char* key, int value) {
 
 const char* itsd_last_error(void) { return g_err.c_str(); }
 
+int itsd_calibrate(int what, double* value, void* stream) {
+  if (!value) return fail(ITSD_ERR_INVALID, "null argument");
+  if (what != ITSD_CALIB_MFMA_BF16 && what != ITSD_CALIB_HBM_COPY) return fail(ITSD_ERR_INVALID, "unknown calibration");
+  const int rc = calibrate_run(what, value, (hipStream_t)stream);
+  if (rc == ITSD_ERR_OOM) return fail(rc, "calibration buffers (2 x 1 GiB)");
+  if (rc != ITSD_OK) return fail(rc, "calibration kernel");
+  return ITSD_OK;
+}
+
 int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value) {
   if (!u || !key || !value) return fail(ITSD_ERR_INVALID, "null argument");
   if (!std::strcmp(key, "graph_captures")) *value = u->graph_captures;
@@ -1354,6 +1339,12 @@ int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value) {
   else if (!std::strcmp(key, "T_sched")) *value = u->T_sched;
   else if (!std::strcmp(key, "ws_bytes")) *value = (int64_t)u->ws_bytes;
   else if (!std::strcmp(key, "ops")) *value = (int64_t)u->ops.size();
+  else if (!std::strcmp(key, "status")) {  // synchronous: the in-kernel hand-off status word of the last forward / run
+    if (hipStreamSynchronize(u->stream) != hipSuccess) return fail(ITSD_ERR_HIP, "status: stream synchronize");
+    int flag = 0;
+    if (hipMemcpy(&flag, u->d_nan + 1, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(ITSD_ERR_HIP, "status: copy");
+    *value = flag;
+  }
   else return fail(ITSD_ERR_INVALID, std::string("unknown query key ") + key);
   return ITSD_OK;
 }
@@ -1443,6 +1434,7 @@ int itsd_unet_forward(itsd_unet* u, const float* x, const int32_t* t, const int3
   c.temb = u->proj_buf; c.tsel = nullptr; c.temb_img_stride = u->sumC;
   c.labels = labels; c.label_mod = n; c.uncond_from = -1;
   c.tail.n = n; c.tail.cfg = 0; c.tail.step_mode = 0; c.tail.eps_out = eps;
+  HIPCHK(hipMemsetAsync(u->d_nan + 1, 0, 4, s));  // this forward's hand-off status (itsd_unet_query "status")
   CHK(run_program(u, c, s));
   u->last_forward_n = n;
   HIPCHK(hipEventRecord(u->ev_out, s));
@@ -1500,6 +1492,7 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
   CHK(check_batch(u, n));
   if (t_begin >= u->T_sched || t_end < 0 || t_end > t_begin) return fail(ITSD_ERR_INVALID, "bad step range");
   HIPCHK(hipSetDevice(u->device));
+  u->last_forward_n = 0;  // (the tail input is overwritten: itsd_unet_representation refuses until the next forward)
   hipStream_t cs = (hipStream_t)stream;
   hipStream_t s = u->stream;
   HIPCHK(hipEventRecord(u->ev_in, cs));
@@ -1558,9 +1551,10 @@ int itsd_sampler_run(itsd_unet* u, float* x, const int32_t* labels, int n, int t
   HIPCHK(hipStreamWaitEvent(cs, u->ev_out, 0));
   if (flags & ITSD_RUN_SYNC) {
     HIPCHK(hipStreamSynchronize(s));
-    int flag = 0;
-    HIPCHK(hipMemcpy(&flag, u->d_nan, 4, hipMemcpyDeviceToHost));
-    if (flag) return fail(ITSD_ERR_NAN, "nan in tensor.");
+    int flag[2] = {0, 0};
+    HIPCHK(hipMemcpy(flag, u->d_nan, 8, hipMemcpyDeviceToHost));
+    if (flag[1]) return fail(ITSD_ERR_HANDOFF, handoff_msg(flag[1]));
+    if (flag[0]) return fail(ITSD_ERR_NAN, "nan in tensor.");
   }
   return ITSD_OK;
 }
@@ -1592,7 +1586,8 @@ int itsd_attention(const void* qkv, const void* vt, void* out, int n, int S, int
     if (C % 8) return fail(ITSD_ERR_INVALID, "C must be a multiple of 8");
     if (vt) {
       if (S % 16 || C % 64 || (S > 256 && !attn_flash_ok(S, C) && !attn_cs_ok(S, C)))
-        return fail(ITSD_ERR_INVALID, "MFMA attention needs S % 16 == 0, C % 64 == 0 (S > 256: C in {64,128,256})");
+        return fail(ITSD_ERR_INVALID, "MFMA attention needs S % 16 == 0, C % 64 == 0 (S > 256: S % 32 == 0 with C in "
+                                      "{64,128,256}, or S % 64 == 0 with C in {256,384,512,1024})");
       a.vt = vt;
     }
     HIPCHK(launch_attn<bf16_t>(a, n, (hipStream_t)stream));
@@ -1617,6 +1612,7 @@ int itsd_profile_forward(itsd_unet* u, const float* x, const int32_t* t, int n, 
   if (u->cfg) return fail(ITSD_ERR_INVALID, "profile_forward: DDPM only");
   CHK(check_batch(u, n));
   HIPCHK(hipSetDevice(u->device));
+  u->last_forward_n = 0;  // (the tail input is overwritten: itsd_unet_representation refuses until the next forward)
   hipStream_t s = u->stream;
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   float* eps = nullptr;
@@ -1662,6 +1658,7 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
   if (op_index < 1 || op_index > (int)u->ops.size()) return fail(ITSD_ERR_INVALID, "profile_op: op_index out of range");
   CHK(check_batch(u, n));
   HIPCHK(hipSetDevice(u->device));
+  u->last_forward_n = 0;  // (the tail input is overwritten: itsd_unet_representation refuses until the next forward)
   hipStream_t s = u->stream;
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   float* eps = nullptr;
@@ -1706,6 +1703,7 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
   if (!u || !x || !t || !n_ops) return fail(ITSD_ERR_INVALID, "null argument");
   CHK(check_batch(u, n));
   HIPCHK(hipSetDevice(u->device));
+  u->last_forward_n = 0;  // (the tail input is overwritten: itsd_unet_representation refuses until the next forward)
   hipStream_t s = u->stream;
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   float* eps = nullptr;
@@ -1752,6 +1750,9 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
         sh[3] = out.H;
         sh[4] = o.ksize;
         sh[5] = o.stride * 10 + o.upsample;
+        // flags for the algorithmic-bytes count (bench.py conv_alg_bytes): bit 0 a residual operand, bit 1 the
+        // output's GroupNorm statistics written, bit 2 the input GroupNorm(+SiLU) fused (its statistics read)
+        sh[7] = (o.resid >= 0 ? 1 : 0) | (out.stats != SIZE_MAX ? 2 : 0) | (o.coef != SIZE_MAX ? 4 : 0);
       }
     }
     ++k;

@@ -11,18 +11,13 @@ extern int g_small_conv;   // 64x64-tile conv_small for small levels (itsd_set_o
 extern int g_splitk;        // split-K on/off (itsd_set_option "splitk")
 extern int g_conv_dbg;      // measurement-only conv switches (itsd_set_option "conv_dbg")
 extern int g_gn_wide;       // 256-pixel fused GroupNorm conv (itsd_set_option "gn_wide")
-extern int g_gn_reg;        // its weights-in-registers variant (itsd_set_option "gn_reg")
-extern int g_small_korder;  // conv_small K order (itsd_set_option "small_korder")
 extern int g_attn_cs;       // attention output-channel slices (itsd_set_option "attn_cs")
 extern int g_attn_aq;       // attention queries per block (itsd_set_option "attn_aq")
-extern int g_p4_w;
-extern int g_p4_m16;        // 16x16x32 MFMA form of conv3x3_gn_p4_kernel (itsd_set_option "p4_m16")          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
+extern int g_p4_w;          // conv3x3_gn_p4_kernel level mask (itsd_set_option "p4_w")
 extern int g_num_cus;       // compute units of the device (persistent grids)
-extern int g_conv_wide;     // 256-pixel plain conv (itsd_set_option "conv_wide")
 extern int g_splitk_inl;     // conv_pipe split-K combined in-launch: 0 off (second launch), 1 on (itsd_set_option "splitk_inl")
 extern int g_p4_plain;      // plain (no GroupNorm) 3x3 stride-1 convs on conv3x3_gn_p4_kernel<W, 2>: 0 off, 1 on (itsd_set_option "p4_plain")
 extern int g_conv1x1;        // streaming 1x1 conv kernel: 0 off, 1 on ("conv1x1")
-extern int g_tail_px;        // tail_mfma_kernel output pixels a block: 128 or 64 ("tail_px")
 extern int g_small_8x8;      // conv_small (split K) for under-filled 8x8-level convs ("small_8x8")
 extern int g_small_wide;     // conv_small for under-filled statistics-free convs of larger images ("small_wide")
 extern int g_attn_wide_nq;   // its query groups a block: 0 auto, 1 / 2 forced ("attn_wide_nq")
@@ -30,9 +25,11 @@ extern int g_attn_wide;      // channel-split attention: 0 off, 1 auto, 2 wherev
 extern int g_small_minks;  // conv_small split K: >= this many K-chunks a slice ("small_minks")
 extern int g_convt_prune;  // ConvTranspose2d sub-pixel phases skip their all-zero taps: 0 off, 1 on ("convt_prune")
 extern int g_subpix_split;  // under-filled sub-pixel conv_pipe launches split K in-launch: 0 off, 1 on ("subpix_split")
+extern int g_p4_xcd;        // persistent fused convs: contiguous tile ranges per XCD ("p4_xcd")
 extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
+extern int g_spin_bound;     // polls before an in-kernel hand-off wait fails: ITSD_ERR_HANDOFF ("spin_bound", diagnostic)
 extern int g_attn_split;     // attn_block_split_kernel at small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
 extern int g_fuse_gn;       // fused GroupNorm+SiLU+conv3x3 in ResBlocks (itsd_set_option "fuse_gn", read at create)
@@ -117,8 +114,6 @@ struct ConvArgs {
   int zins;                          // zero-insertion (ConvTranspose2d s2 as a gather conv, ModelCondition.py:80)
   const void* wt;                    // packed [Cout][K], K = ksize*ksize*(C1+C2), k=(ky*ks+kx)*Cin+ci
   const void* wfrag;                 // the same weights in MFMA A-fragment order [Cout/32][K/16][64][8]
-  const void* wfrag16;               // ... in v_mfma_f32_16x16x32_bf16 A-fragment order [Cout/16][K/32][64][8]
-                                     // (fused GroupNorm convs, bf16), or null
   int Cout, K;
   const float* bias;                 // [Cout]
   // epilogue additive vectors (ResBlock temb_proj, Model.py:204; CFG cond_proj ModelCondition.py:156)
@@ -147,6 +142,7 @@ struct ConvArgs {
                                      // (grid.z = phase py*2+px): Hout/Wout/M/ksize/K describe the
                                      // input-grid GEMM; output rows are (2i+py, 2j+px) of a 2x grid
   int dbg;                           // g_conv_dbg (measurements only)
+  int xcd;                           // persistent fused convs: deal each XCD a contiguous range of tiles (speed only)
   int tap_live;                      // subpix 2 on conv3x3_gn_p4_kernel: skip each phase's all-zero taps
                                      // (conv_pipe runs all 9: measured no faster with live taps)
   // conv3x3_gn_p5_kernel (the fused conv of the 8x8 / 4x4 levels): K split into ksplit slices
@@ -211,6 +207,8 @@ struct AttnBlockArgs {
   float* spart;           // [n][G][4 tiles][64 lanes][16] fp32
   bf16_t* oslab;          // [n][64][C] bf16
   int* sync;              // [n][2], never reset (targets from each block's own add)
+  int* err;               // device status word: bit 0 set when a hand-off wait exhausted its poll bound
+  int spin_bound;         // polls before a hand-off wait gives up (itsd_set_option "spin_bound", diagnostic)
 };
 
 struct HeadArgs {

@@ -39,7 +39,7 @@ constexpr int EPI_BYTES = 128 * EROW * 4 + 8 * 2 * 128 * 4;  // fp32 tile + stat
 constexpr int SMEM_BYTES = (2 * 2 * TILEB > EPI_BYTES) ? 2 * 2 * TILEB : EPI_BYTES;
 int g_fuse_gn = 1;
 int g_conv_dbg = 0;
-int g_conv_variant = 2;  // 0 pipe 4 stages, 1 register-staged, 2/3 pipe with 2/3 stages
+int g_conv_variant = 2;  // 2 conv_pipe (2-stage LDS-DMA ring), 1 conv_igemm (register-staged)
 int g_small_conv = 1;    // 64x64-tile conv for the small levels: 0 off, 1 auto, 2 whenever eligible
 int g_conv1x1 = 1;       // streaming 1x1 kernel for statistics-free 1x1 convs of large pixel counts: 0 off,
                          // 1 on (4-stage ring), 2 on (7-stage ring) ("conv1x1")
@@ -48,12 +48,8 @@ int g_small_wide = 1;    // ... also for statistics-free convs of larger images 
                          // whose 128x128 conv_pipe grid under-fills the chip (small batches) ("small_wide")
 int g_splitk = 1;        // split-K for under-filled grids (variant 2): 0 off, 1 auto, >= 2 forced slices
 int g_gn_wide = 1;       // 256-pixel fused GroupNorm conv: 0 off, 1 auto, 2 whenever eligible
-int g_gn_reg = 4;        // the 256-pixel fused GroupNorm conv: 4 = conv3x3_gn_p4_kernel (the only shipped
-                         // generation; the superseded 0-3 were deleted in round 4)
-int g_small_korder = 0;  // conv_small K order: 1 taps inside each 64-channel chunk, 0 tap-major (default: 1 measured 2-3 % slower)
-int g_p4_w = 7;          // levels conv3x3_gn_p4_kernel takes: bit 0 W = 8, 1 W = 16, 2 W = 32, 3 W = 64 (off:
-                         // at C4's N = 16, 1 tile a CU, 34.8 vs 33.0 us a launch on p5, profiles/r04/census_c4_p4_64*)
-int g_p4_m16 = 0;        // conv3x3_gn_p4_kernel's 16x16x32 MFMA form at W = 32 / 16 (A/B switch)
+int g_p4_w = 7;          // levels conv3x3_gn_p4_kernel takes: bit 0 W = 8, 1 W = 16, 2 W = 32 (64x64 runs p5: p4 there
+                         // measured 34.8 vs 33.0 us a launch at C4's N = 16, profiles/r04/census_c4_p4_64*; removed in round 5)
 int g_num_cus = 256;     // compute units of the device (set at itsd_unet_create): persistent grids
 int g_splitk_inl = 1;     // conv_pipe split-K combined in-launch (ticket) instead of splitk_epilogue_kernel
 int g_p4_plain = 1;      // plain 3x3 stride-1 convs (the CFG upsample's conv) on conv3x3_gn_p4_kernel<W, 2>
@@ -61,12 +57,11 @@ int g_small_minks = 8;    // conv_small split K: >= this many K-chunks a slice (
                           // 2: N=32 step -2.3 %, N=64 -0.9 %, N=256 / C3 / C4 equal, profiles/r04/small_minks_ab.txt)
 int g_convt_prune = 1;    // ConvTranspose2d sub-pixel phases skip their all-zero taps (itsd_set_option "convt_prune")
 int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
+int g_p4_xcd = 0;        // conv3x3_gn_p4_kernel: each XCD a contiguous range of tiles (ConvArgs::xcd)
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
-int g_conv_wide = 0;     // (round 3's 256-pixel plain conv, measured slower than conv_pipe / conv_small and
-                         // deleted in round 4: only 0 is accepted)
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
@@ -1431,9 +1426,6 @@ template <int W> struct GnpCfg;
 template <> struct GnpCfg<32> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<16> { static constexpr int NSEG = 1, ITEMS = 11, RES = 1; };
 template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 0; };  // LDS: residual from HBM
-// 64x64 (C4's level 0): 4-row tiles, a 6 x 66-row halo (13 items of 32 rows) -- two halo buffers leave
-// no room for the residual tile, so the register epilogue reads it from HBM as at 8x8
-template <> struct GnpCfg<64> { static constexpr int NSEG = 1, ITEMS = 13, RES = 0; };
 
 
 // ---------------------------------------------------------------------------- persistent, one MFMA wave per SIMD
@@ -1447,11 +1439,6 @@ template <> struct GnpCfg<64> { static constexpr int NSEG = 1, ITEMS = 13, RES =
 constexpr int P4_RING = 6;  // A k-step slots (prefetch distance 5 k-steps = 40 MFMAs); divides the 36 k-steps
                             // of a chunk, so the slots of the next chunk's prefetched steps line up
 constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 MFMAs ahead)
-// M16: the MFMA waves run v_mfma_f32_16x16x32_bf16 (4 x 8 tiles of 16 couts x 16 pixels per wave,
-// 32 MFMAs per 32-deep k-step; weights from wfrag16), the same work per instruction cycle as
-// 32x32x16 but a denser-clocking shape (MI355X_MICROARCH.md, DVFS item 7); RES configurations
-// (W = 32, 16) only. The halo waves are the same.
-constexpr int P16_RING = 2;  // A k32-step slots (divides the 18 k32-steps of a chunk)
 // AB: bit 1 (value 2) = plain conv3x3 (no GroupNorm+SiLU: the halo waves copy the input; shipped, the
 // CFG UpSample's 3x3 conv, conv_p4_plain_selected); bit 7 (value 128) = a sub-pixel phase conv (plain):
 // W is the INPUT grid, a tile is (phase, 256 input-grid pixels, 128 couts) with the phase's weights
@@ -1460,7 +1447,7 @@ constexpr int P16_RING = 2;  // A k32-step slots (divides the 18 k32-steps of a 
 // upsample + conv3x3 (Model.py:121-126, the phase's 2x2 folded taps), or with bit 8 (value 256) the 9
 // taps of a 3x3 window for ConvTranspose2d(5, 2, 2, 1) (ModelCondition.py:80, the phase's taps of the 5x5
 // kernel) (conv_p4_sub_selected); the other bits are diagnostic ablations (ITSD_DIAG).
-template <int W, int AB = 0, bool M16 = false>
+template <int W, int AB = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   typedef bf16_t T;
   constexpr bool SUB = (AB & 128) != 0, PLAIN = SUB || (AB & 2) != 0;
@@ -1477,7 +1464,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // (sub-pixel forms: 4 slots, dividing every phase's k-step count: 16, or 36 / 24 / 24 / 16 live)
   constexpr int RING = ((AB & 64) || SUB) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
   static_assert(KST % RING == 0, "ring slots repeat per chunk");
-  static_assert(!(SUB && M16), "the sub-pixel form runs the 32x32x16 MFMA path");
   // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]
   __shared__ __attribute__((aligned(16))) char smem[2 * HALO + RESB + 2 * NSEG * CONV_BM * 4 + 4 * 64 * 4];
   char* const rlds = smem + 2 * HALO;
@@ -1493,7 +1479,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int H = a.Hout;
   const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
   const int nTC = a.Cout / CONV_BM, nPT = a.M / GNW_BN, NT = (SUB ? 4 : 1) * nPT * nTC;
-  const int G = gridDim.x, b = blockIdx.x;
+  // xcd: blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one; speed only), so logical
+  // block (b % 8) * G/8 + b / 8 gives each XCD a contiguous eighth of the tile sequence: the cout tiles of a
+  // pixel tile (8x8: 3 blocks) read its input through one L2 instead of three
+  const int G = gridDim.x;
+  const int b = (a.xcd && (G & 7) == 0) ? (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   // block b walks the contiguous tile range [tb0, tb0 + ntiles) (cout tile fastest): its tiles share
   // pixel tiles and images, so a gn_fold block reduces an image's statistics once for all of them
   const int tb0 = (int)(((long long)b * NT) / G);
@@ -1568,130 +1558,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     }
   };
 
-  if (M16 && wid < 4) {
-    if constexpr (M16) {
-      static_assert(RES, "the 16x16x32 path drains through the LDS output tile");
-      // wave (wm, wn): couts 64 wm + 16 mt + 4 kq + r (mt < 4, r < 4), pixels 128 wn + 16 nt + c16
-      // (nt < 8); lane (c16, kq) reads B rows of its pixel, channels 32 h + 8 kq .. +7 of the chunk
-      const int wm = wid & 1, wn = wid >> 1, c16 = lane & 15, kq = lane >> 4;
-      int hb[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int pl = wn * 128 + j * 16 + c16;
-        const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-        hb[j] = seg * HS + oy * W2 + (rem - oy * W);
-      }
-      const int kp32 = Cin >> 5;
-      const size_t ablk = (size_t)(9 * kp32) * 1024;  // one 16-cout block of fragments
-      auto abase_of = [&](int k) {
-        return (const char*)a.wfrag16 + (size_t)((tile_c(k) >> 4) + 4 * wm) * ablk + lane * 16;
-      };
-      f32x4 acc[4][8];
-      u32x4 ra[P16_RING][4];
-      auto load_a = [&](const char* base, int st, u32x4 (&dst)[4]) __attribute__((always_inline)) {
-        const size_t off = (size_t)((st >> 1) * kp32 + (st & 1)) * 1024;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) dst[m] = *(const u32x4*)(base + m * ablk + off);
-      };
-      {
-        const char* ab0 = abase_of(0);
-#pragma unroll
-        for (int s0 = 0; s0 < P16_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
-      }
-      auto init_acc = [&](int kk) __attribute__((always_inline)) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const f32x4 ad = *(const f32x4*)(addv + (kk & 1) * CONV_BM + wm * 64 + mt * 16 + 4 * kq);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[mt][j] = ad;
-        }
-      };
-      stage_addv(0, tid);
-      block_sync();  // B0: stage 0 staged
-      init_acc(0);
-      int q = 0;
-      for (int k = 0; k < ntiles; ++k) {
-        const char* ab = abase_of(k);
-        const char* abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
-        for (int cc = 0; cc < ncc; ++cc, ++q) {
-          const char* hcur = smem + (q & 1) * HALO;
-          const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 2 * 1024 : (k + 1 < ntiles ? abn : ab);
-          const char* cb = ab + (size_t)cc * 2 * 1024;
-          STAMP(c0);
-          // 18 k32-steps (9 taps x 2); B fragment j of step st at byte tb[j] ^ ((st & 1) << 6),
-          // tb[j] = row * 128 + ((kq ^ sw(row)) << 4) rebuilt per tap
-          int tb[8];
-          bf16x8 fb[8];
-          auto taprows = [&](int tap) __attribute__((always_inline)) {
-            const int ky = tap / 3, kx = tap - ky * 3;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              int h = hb[j] + ky * W2 + kx;
-              asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
-              tb[j] = (int)(hcur - smem) + h * ROWB + ((kq ^ ((h >> 1) & 7)) << 4);
-            }
-          };
-          auto rd = [&](int st, int j0) __attribute__((always_inline)) {
-#pragma unroll
-            for (int j = j0; j < j0 + 4; ++j) fb[j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 1) << 6)));
-          };
-          taprows(0);
-          rd(0, 0);
-          rd(0, 4);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int step = 0; step < 18; ++step) {
-            const int pf = step + P16_RING - 1;
-            if (pf < 18) load_a(cb, pf, ra[pf % P16_RING]);
-            else load_a(nb, pf - 18, ra[pf % P16_RING]);
-            if (step + 1 < 18 && ((step + 1) & 1) == 0) taprows((step + 1) >> 1);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-#pragma unroll
-              for (int j = 4 * half; j < 4 * half + 4; ++j)
-#pragma unroll
-                for (int mt = 0; mt < 4; ++mt)
-                  acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[step % P16_RING][mt]),
-                                                                      fb[j], acc[mt][j], 0, 0, 0);
-              if (step + 1 < 18) rd(step + 1, 4 * half);  // this half's B of the next step
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-          STAMP(c1);
-          STAMP_ADD(0, c1 - c0);
-          block_sync();  // end of stage q
-        }
-        STAMP(e0);
-        // epilogue of tile k: out = acc (from addv) + residual, rounded into the LDS tile in place
-        // of the residual (8 B per lane and tile); the halo waves drain it
-        {
-          const bool hr = a.resid != nullptr;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int p = wn * 128 + j * 16 + c16;
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-              char* e = rlds + wm * 32768 + p * 128 + (((2 * mt + (kq >> 1)) ^ ((p >> 1) & 7)) << 4) + 8 * (kq & 1);
-              uint2 r = *(const uint2*)e;
-              if (!hr) r = uint2{0u, 0u};
-              const float v0 = acc[mt][j][0] + __uint_as_float(r.x << 16);
-              const float v1 = acc[mt][j][1] + __uint_as_float(r.x & 0xffff0000u);
-              const float v2 = acc[mt][j][2] + __uint_as_float(r.y << 16);
-              const float v3 = acc[mt][j][3] + __uint_as_float(r.y & 0xffff0000u);
-              *(uint2*)e = uint2{pk_bf16(v0, v1), pk_bf16(v2, v3)};
-            }
-          }
-        }
-        if (k + 1 < ntiles) init_acc(k + 1);
-        STAMP(e1);
-        STAMP_ADD(6, e1 - e0);
-      }
-      block_sync();  // the last tile's output is in LDS
-      P4_STAMP_OUT();
-      return;
-    }
-  }
   if (wid < 4) {
     // ================================================================ MFMA waves (one per SIMD)
     // wave w: couts 64*(w & 1) .. +63 (two 32-cout A fragments per k-step), pixels 128*(w >> 1) ..
@@ -1704,9 +1570,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
       hb[j] = seg * HS + oy * W2 + (rem - oy * W);
     }
-    const size_t ablk = (size_t)(NTAP * kpt) * 1024;  // one 32-cout block of fragments
-    auto abase_of = [&](int k) {
-      return (const char*)a.wfrag + ((size_t)tile_ph(k) * (a.Cout >> 5) + (tile_c(k) >> 5) + 2 * wm) * ablk + lane * 16;
+    const uint32_t ablk = (uint32_t)(NTAP * kpt) * 1024;  // one 32-cout block of fragments
+    // A fragments by buffer loads: resource = the whole wfrag array, voffset = this lane's 16 B of the wave's
+    // two 32-cout blocks, soffset = the tile's fragment block + the k-step (uniform: scalar arithmetic, no
+    // 64-bit address VGPRs, no per-step 64-bit SGPR offsets held across the chunk loop)
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wfrag, (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t avo0 = (uint32_t)lane * 16 + 2 * wm * ablk, avo1 = avo0 + ablk;
+    auto abase_of = [&](int k) -> uint32_t {
+      return (uint32_t)(tile_ph(k) * (a.Cout >> 5) + (tile_c(k) >> 5)) * ablk;
     };
     f32x16 acc[2][4];
 #pragma unroll
@@ -1716,29 +1587,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
     u32x4 ra[RING][2];
-    auto load_a = [&](const char* base, int st, u32x4 (&dst)[2]) __attribute__((always_inline)) {
-      const size_t off = (size_t)((st >> 2) * kpt + (st & 3)) * 1024;
+    auto load_a = [&](uint32_t base, int st, u32x4 (&dst)[2]) __attribute__((always_inline)) {
+      const uint32_t off = base + (uint32_t)((st >> 2) * kpt + (st & 3)) * 1024;
       if constexpr ((AB & 8) != 0) {
         dst[0] = u32x4{(uint32_t)st, 0u, 0u, 0u};
         dst[1] = u32x4{(uint32_t)st, 1u, 0u, 0u};
       } else {
-        dst[0] = *(const u32x4*)(base + off);
-        dst[1] = *(const u32x4*)(base + ablk + off);
+        dst[0] = __builtin_amdgcn_raw_buffer_load_b128(wrs, avo0, off, 0);
+        dst[1] = __builtin_amdgcn_raw_buffer_load_b128(wrs, avo1, off, 0);
       }
     };
     // ConvTranspose2d phases with tap_live: a chunk runs only its phase's live taps; the A prefetch that
     // crosses into the next chunk / tile starts at that chunk's first live tap (tap0_off)
-    auto tap0_off = [&](int k) -> size_t {
+    auto tap0_off = [&](int k) -> uint32_t {
       if constexpr (CT) {
         if (a.tap_live) {
           const int ph = tile_ph(k);
-          return (size_t)(((ph >> 1) * 3 + (ph & 1)) * kpt) * 1024;
+          return (uint32_t)(((ph >> 1) * 3 + (ph & 1)) * kpt) * 1024;
         }
       }
       return 0;
     };
     {
-      const char* ab0 = abase_of(0) + tap0_off(0);
+      const uint32_t ab0 = abase_of(0) + tap0_off(0);
 #pragma unroll
       for (int s0 = 0; s0 < RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
     }
@@ -1762,13 +1633,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     int q = 0;     // stage (chunk) counter of this block
     for (int k = 0; k < ntiles; ++k) {
       const int tileP = tile_p(k), tileC = tile_c(k), tph = tile_ph(k);
-      const char* ab = abase_of(k);
-      const char* abn = k + 1 < ntiles ? abase_of(k + 1) + tap0_off(k + 1) : ab;
-      const size_t t0k = tap0_off(k);
+      const uint32_t ab = abase_of(k);
+      const uint32_t abn = k + 1 < ntiles ? abase_of(k + 1) + tap0_off(k + 1) : ab;
+      const uint32_t t0k = tap0_off(k);
       for (int cc = 0; cc < ncc; ++cc, ++q) {
         const char* hcur = smem + (q & 1) * HALO;
-        const char* nb = cc + 1 < ncc ? ab + (size_t)(cc + 1) * 4 * 1024 + t0k : (k + 1 < ntiles ? abn : ab);
-        const char* cb = ab + (size_t)cc * 4 * 1024;
+        const uint32_t nb = cc + 1 < ncc ? ab + (uint32_t)(cc + 1) * 4 * 1024 + t0k : (k + 1 < ntiles ? abn : ab);
+        const uint32_t cb = ab + (uint32_t)cc * 4 * 1024;
         STAMP(c0);
         // the step's A loads, B reads and address VALU spread over its 8 MFMA gaps (measured against all of
         // them ahead of the MFMAs in one gap: 32x32 -1 %, 16x16 -3 %, 8x8 -1.5 %, profiles/r03b/p4_sgb_ab.txt)
@@ -1837,8 +1708,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
             const bool last = ti + 1 == ntl;
             const int nky = kx == 2 ? ky + 1 : ky, nkx = kx == 2 ? rx : kx + 1;
             const int rky = last ? ky : nky, rkx = last ? kx : nkx;  // (the last tap re-reads its own rows)
-            const char* tcur = cb + (size_t)((ky * 3 + kx) * kpt) * 1024;
-            const char* tnxt = last ? nb : cb + (size_t)((nky * 3 + nkx) * kpt) * 1024;
+            const uint32_t tcur = cb + (uint32_t)((ky * 3 + kx) * kpt) * 1024;
+            const uint32_t tnxt = last ? nb : cb + (uint32_t)((nky * 3 + nkx) * kpt) * 1024;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
               if (kk == 0) load_a(tcur, 3, ra[3]);
@@ -2183,6 +2054,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // sum (b3 = 0) or sum of squares of couts 8u + 4 b4 + 2 b5 + {0, 1}
   auto drain = [&](int kd) __attribute__((always_inline)) {
     if constexpr (RES) {
+      // (lane from an opaque copy: the row / unit addresses are rebuilt per call, not held in registers
+      // across the whole stage loop for the final drain -- they spilled to scratch)
+      int lane = tid & 63;
+      asm volatile("" : "+v"(lane));
       const int tileP = tile_p(kd), tileC = tile_c(kd), u = lane & 7, dph = tile_ph(kd);
       float v[16];
 #pragma unroll
@@ -2475,25 +2350,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       const int pl = j * 32 + rl, seg = pl / SPX, rem = pl - seg * SPX, y = rem / W;
       hb[j] = seg * HS + y * W2 + (rem - y * W);
     }
-    const size_t ablk = (size_t)(9 * kpt) * 1024;  // one 32-cout block of fragments
-    auto abase = [&](int tc, int cc) {
-      return (const char*)a.wfrag + (size_t)(tc * 4 + wid) * ablk + (size_t)cc * 4 * 1024 + lane * 16;
-    };
-    auto load_a = [&](const char* base, int st, u32x4& dst) __attribute__((always_inline)) {
+    const uint32_t ablk = (uint32_t)(9 * kpt) * 1024;  // one 32-cout block of fragments
+    // A fragments by buffer loads (conv3x3_gn_p4_kernel's scheme): voffset = this lane's 16 B of the wave's
+    // 32-cout block, soffset = the tile's fragment block + chunk + k-step (uniform scalar arithmetic)
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wfrag, (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t avo = (uint32_t)lane * 16 + (uint32_t)wid * ablk;
+    auto abase = [&](int tc, int cc) -> uint32_t { return (uint32_t)(tc * 4) * ablk + (uint32_t)cc * 4 * 1024; };
+    auto load_a = [&](uint32_t base, int st, u32x4& dst) __attribute__((always_inline)) {
 #if defined(ITSD_DIAG) && defined(P5_AB)
       if constexpr ((P5_AB & 8) != 0) {  // ablation: no A loads
         dst = u32x4{(uint32_t)st, 0u, 0u, 0u};
         return;
       }
 #endif
-      dst = *(const u32x4*)(base + (size_t)((st >> 2) * kpt + (st & 3)) * 1024);
+      dst = __builtin_amdgcn_raw_buffer_load_b128(wrs, avo, base + (uint32_t)((st >> 2) * kpt + (st & 3)) * 1024, 0);
     };
     f32x16 acc[4];
     u32x4 ra[P5_RING];
     {
       int tp, tc, z;
       item_of(0, tp, tc, z);
-      const char* ab0 = abase(tc, chunk_lo(z));
+      const uint32_t ab0 = abase(tc, chunk_lo(z));
 #pragma unroll
       for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
     }
@@ -2515,7 +2392,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[j][r] = 0.0f;
 #endif
-      const char* nitem = nullptr;  // the next item's first chunk (A prefetch across the item boundary)
+      uint32_t nitem = abase(tc, c1 - 1);  // the next item's first chunk (A prefetch across the item boundary)
       if (k + 1 < nit) {
         int tp2, tc2, z2;
         item_of(k + 1, tp2, tc2, z2);
@@ -2523,8 +2400,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       }
       for (int cc = c0; cc < c1; ++cc, ++q) {
         const char* hcur = smem + (q & 1) * HALO;
-        const char* cb = abase(tc, cc);
-        const char* nb = cc + 1 < c1 ? abase(tc, cc + 1) : (nitem ? nitem : cb);
+        const uint32_t cb = abase(tc, cc);
+        const uint32_t nb = cc + 1 < c1 ? abase(tc, cc + 1) : nitem;
         int tb[4];
         bf16x8 fb[P5_BD][4];
         auto rd = [&](int st, int buf) __attribute__((always_inline)) {
@@ -3191,7 +3068,7 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false) {
   int segs = 0;
   if (GNW_BN / W <= H) {
     const int THs = GNW_BN / W;
-    const int items = W == 64 ? GnpCfg<64>::ITEMS : GnpCfg<32>::ITEMS;  // p4's halo items (32 rows each)
+    const int items = GnpCfg<32>::ITEMS;  // p4's halo items (32 rows each)
     if (H % THs == 0 && (THs + 2) * (W + 2) <= items * 32) segs = 1;
   } else if (GNW_BN == 4 * H * W && (H + 2) * (W + 2) <= GnpCfg<8>::ITEMS * 8) {
     segs = 4;
@@ -3227,9 +3104,8 @@ bool conv_p5_selected(const ConvArgs& a);
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p4_kernel (any form)?
 bool conv_p4_selected(const ConvArgs& a) {
   if (!a.gn_coef || conv_p5_selected(a) || !conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
-  return g_gn_reg == 4 && a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
-         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)) ||
-          (a.Wout == 64 && (g_p4_w & 8)));
+  return a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
+         ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
 }
 
 // A plain (no GroupNorm) 3x3 stride-1 conv on conv3x3_gn_p4_kernel<W, 2>? (the CFG UpSample's conv
@@ -3263,7 +3139,7 @@ bool conv_p5_selected(const ConvArgs& a) {
   if (!a.gn_coef || !a.wfrag || a.Cout % CONV_BM || a.C1 % 64 || a.C2 % 64 || !p5_eligible(a.Hout, a.Wout)) return false;
   const int p4_tiles = (a.M % GNW_BN) ? 0 : (a.M / GNW_BN) * (a.Cout / CONV_BM);
   // (4x4: no other persistent fused kernel holds it; 64x64 on p5 unless p4_w bit 3 is set)
-  return a.Wout == 4 || (a.Wout == 64 && !(g_p4_w & 8)) || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
+  return a.Wout == 4 || a.Wout == 64 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
 }
 
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
@@ -3316,11 +3192,8 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
 #ifdef ITSD_DIAG
           if ((g_conv_dbg & 4096) && a.Wout == 32) return launch_p4_ablation(a, gp, s);
 #endif
-          if (g_p4_m16 && a.wfrag16 && a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p4_kernel<32, 0, true>), gp, dim3(512), 0, s, a);
-          else if (g_p4_m16 && a.wfrag16 && a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p4_kernel<16, 0, true>), gp, dim3(512), 0, s, a);
-          else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p4_kernel<32>, gp, dim3(512), 0, s, a);
+          if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p4_kernel<32>, gp, dim3(512), 0, s, a);
           else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p4_kernel<16>, gp, dim3(512), 0, s, a);
-          else if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p4_kernel<64>, gp, dim3(512), 0, s, a);
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }
@@ -3391,8 +3264,7 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
         (g_small_conv == 2 || S > 1 || wide || small8 ||
          (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
       gs.z = S;
-      if (g_small_korder) ITSD_LAUNCH(conv_small<true>, gs, dim3(256), 0, s, a);
-      else ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
+      ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }
@@ -3430,11 +3302,9 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       while (S > 1 && (long long)blocks * S * 16384 > a.splitk_cap) --S;
       if (S > 1) grid.z = 4 * S;
     }
-    // (conv_variant 3 / 0: 3- / 4-stage rings at one block a CU, measured 8-30 % slower here,
+    // (3- / 4-stage rings at one block a CU measured 8-30 % slower here and were removed in round 5,
     // profiles/r04/census_archC_2N64_conv_variant*.txt)
-    if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, a);
-    else if (v == 0) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, a);
-    else ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
+    ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
   ConvArgs b = a;  // (conv_pipe's split-K: in-launch combine unless the tiles outnumber the tickets)
@@ -3451,12 +3321,8 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     grid.z = S < 1 ? 1 : S;
   }
   if (!pipe || v == 1) ITSD_LAUNCH(conv_igemm<T>, grid, dim3(256), 0, s, a);
-  else if (v == 2 && lin) ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, b);
-  else if (v == 2) ITSD_LAUNCH((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, b);
-  else if (v == 3 && lin) ITSD_LAUNCH((conv_pipe<T, 3, true>), grid, dim3(256), 0, s, b);
-  else if (v == 3) ITSD_LAUNCH((conv_pipe<T, 3, false>), grid, dim3(256), 0, s, b);
-  else if (lin) ITSD_LAUNCH((conv_pipe<T, 4, true>), grid, dim3(256), 0, s, b);
-  else ITSD_LAUNCH((conv_pipe<T, 4, false>), grid, dim3(256), 0, s, b);
+  else if (lin) ITSD_LAUNCH((conv_pipe<T, 2, true>), grid, dim3(256), 0, s, b);
+  else ITSD_LAUNCH((conv_pipe<T, 2, false>), grid, dim3(256), 0, s, b);
   if (grid.z > 1 && pipe && v != 1 && !b.tickets) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

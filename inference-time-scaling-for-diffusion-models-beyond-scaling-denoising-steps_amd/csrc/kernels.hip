@@ -349,22 +349,20 @@ __device__ __forceinline__ void atl(int slot) {
 #define ATL(slot)
 #endif
 
-template <int C, int IPB>
+// (round 4's 4-images-a-block form for the 4x4 middle block, S = 16, measured slower than the unfused ops
+// at N = 32 and equal at N = 256, was removed in round 5)
+template <int C>
 __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
-  // IPB images of SI = 64 / IPB tokens a block (IPB = 4: the 4x4 middle block, S = 16), their 64 tokens
-  // projected together; the scores of a query are masked to its own image's keys
-  constexpr int S = 64, SI = S / IPB, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
-  static_assert(C % 128 == 0 && SI % 16 == 0, "C, SI");
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
+  static_assert(C % 128 == 0, "C");
   constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256, R_ST = R_GS + 32 * 2 * 4;
-  // (IPB > 1: the group statistics of the images live in the V^T region until phase 1, and the
-  // consumer statistics go straight from the lanes to the slab: no R_GS / R_ST)
-  __shared__ __attribute__((aligned(16))) char sm[IPB == 1 ? R_ST + 2 * C * 2 * 4 : R_GS];
+  __shared__ __attribute__((aligned(16))) char sm[R_ST + 2 * C * 2 * 4];
   const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wq = w & 3, wt = w >> 2;  // wave = (channel-block group, token block)
-  const int img = blockIdx.x * IPB, nimg = min(IPB, a.n - img), ntok = nimg * SI;
+  const int img = blockIdx.x;
   ATL(0);
-  const bf16_t* x = a.x + (size_t)img * SI * C;
+  const bf16_t* x = a.x + (size_t)img * S * C;
   // [row][C] bf16 image, 16-B chunk ch of row r at (ch ^ (r & 15))
   auto rowc = [](int r, int ch, int rowbytes) { return r * rowbytes + ((ch ^ (r & 15)) << 4); };
   // [row][64] bf16 image (128-B rows), chunk ch of row r at ch ^ ((r >> 1) & 7)
@@ -378,18 +376,15 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 #pragma unroll
   for (int i = 0; i < XU; ++i) {
     const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8);
-    xv[i] = t < ntok ? *(const u32x4*)(x + (size_t)t * C + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+    xv[i] = *(const u32x4*)(x + (size_t)t * C + ch * 8);
   }
-  float* gs = (float*)(sm + (IPB == 1 ? R_GS : R_VT));  // [image of the block][32 groups][mean, rstd]
-#pragma unroll
-  for (int p2 = 0; p2 < (IPB + 1) / 2; ++p2) {  // two images a pass (threads 0-255, 256-511)
-    const int il = 2 * p2 + (tid >> 8);
-    if (il >= nimg) continue;
-    const int g = (tid >> 3) & 31, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
+  float* gs = (float*)(sm + R_GS);  // [32 groups][mean, rstd]
+  if (tid < 256) {
+    const int g = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
     double s = 0.0, q = 0.0;
     for (int k = l8; k < n_it; k += 8) {
       const int c = g * gsz + k / a.spi;
-      const long long sl = (long long)(img + il) * a.spi + k % a.spi;
+      const long long sl = (long long)img * a.spi + k % a.spi;
       s += (double)a.st[(sl * 2) * C + c];
       q += (double)a.st[(sl * 2 + 1) * C + c];
     }
@@ -399,11 +394,11 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       q += __shfl_xor(q, o, 64);
     }
     if (l8 == 0) {
-      const double E = (double)gsz * SI, mean = s / E;
+      const double E = (double)gsz * S, mean = s / E;
       double var = q / E - mean * mean;
       var = var > 0.0 ? var : 0.0;
-      gs[(il * 32 + g) * 2] = (float)mean;
-      gs[(il * 32 + g) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+      gs[g * 2] = (float)mean;
+      gs[g * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
     }
   }
   __syncthreads();
@@ -417,7 +412,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       float y[2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
-        const int c = c0 + 2 * e2 + h2, g = (IPB == 1 ? 0 : (t / SI) * 32) + c / (C / 32);  // (an 8-channel chunk may straddle two groups)
+        const int c = c0 + 2 * e2 + h2, g = c / (C / 32);  // (an 8-channel chunk may straddle two groups)
         const float mean = gs[2 * g], rstd = gs[2 * g + 1];
         const float sc = rstd * a.gamma[c];
         const float xf = __uint_as_float(h2 ? (xv[i][e2] & 0xffff0000u) : (xv[i][e2] << 16));
@@ -554,7 +549,6 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       v[e] = Sm[qry * (S + 4) + k0 + e];
-      if (IPB > 1 && (k0 + e) / SI != qry / SI) v[e] = -INFINITY;  // another image's key
       m = fmaxf(m, v[e]);
     }
 #pragma unroll
@@ -634,7 +628,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
           if (w + 8 * b < CB) acc[tb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[b], o0, acc[tb][b], 0, 0, 0);
       }
     }
-    bf16_t* out = a.out + (size_t)img * SI * C;
+    bf16_t* out = a.out + (size_t)img * S * C;
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb) {
       const int tk = 32 * tb + rl;  // this lane's token
@@ -648,7 +642,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * cb + 8 * g + 4 * hh;
           const f32x4 bb = *(const f32x4*)(a.bp + c);
-          const uint2 rr = tk < ntok ? *(const uint2*)(x + (size_t)tk * C + c) : uint2{0u, 0u};
+          const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
           const float v0 = acc[tb][b][4 * g + 0] + bb[0] + __uint_as_float(rr.x << 16);
           const float v1 = acc[tb][b][4 * g + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
           const float v2 = acc[tb][b][4 * g + 2] + bb[2] + __uint_as_float(rr.y << 16);
@@ -671,7 +665,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
             o[d] = sw[0];
             o[2 + d] = sw[1];
           }
-          if (tk < ntok) *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
+          *(u32x4*)(out + (size_t)tk * C + 32 * cb + 8 * (gp + hh)) = o;
         }
         if (a.out_stats) {  // this token block's 32 lanes: butterfly, then the two blocks summed in order
           auto xchg = [](float xf, auto wc) {
@@ -693,45 +687,19 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
               v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
             }
           };
-          if constexpr (IPB == 1) {
-            halve(std::integral_constant<int, 16>{});
-            halve(std::integral_constant<int, 8>{});
-            halve(std::integral_constant<int, 4>{});
-            halve(std::integral_constant<int, 2>{});
-            halve(std::integral_constant<int, 1>{});
-            const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
-            spart[(tb * 2 + (rl >> 4)) * C + co] = v[0];
-          } else {
-            // 16-token images: the sums and the squares halved separately over the 16 lanes of an
-            // image (lane bits 0-3), so lane (image rl >> 4, e) ends with channel co's sum and square
-            // sum of its own image, stored straight to that image's slot
-            auto halve2 = [&](auto wc) {
-              constexpr int wd = decltype(wc)::value;
-              const bool up = (rl & wd) != 0;
-#pragma unroll
-              for (int hq = 0; hq < 2; ++hq)
-#pragma unroll
-                for (int ii = 0; ii < wd; ++ii) {
-                  const float lo = v[16 * hq + ii], hi = v[16 * hq + ii + wd];
-                  v[16 * hq + ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
-                }
-            };
-            halve2(std::integral_constant<int, 8>{});
-            halve2(std::integral_constant<int, 4>{});
-            halve2(std::integral_constant<int, 2>{});
-            halve2(std::integral_constant<int, 1>{});
-            const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3), il = tk / SI;
-            if (il < nimg) {
-              a.out_stats[(long long)(img + il) * 2 * C + co] = v[0];
-              a.out_stats[(long long)(img + il) * 2 * C + C + co] = v[16];
-            }
-          }
+          halve(std::integral_constant<int, 16>{});
+          halve(std::integral_constant<int, 8>{});
+          halve(std::integral_constant<int, 4>{});
+          halve(std::integral_constant<int, 2>{});
+          halve(std::integral_constant<int, 1>{});
+          const int e = rl & 15, co = 32 * cb + 8 * (e >> 2) + 4 * hh + (e & 3);
+          spart[(tb * 2 + (rl >> 4)) * C + co] = v[0];
         }
       }
     }
   }
   ATL(6);  // proj + epilogue (wave's own)
-  if (IPB == 1 && a.out_stats) {
+  if (a.out_stats) {
     __syncthreads();
     for (int i = tid; i < 2 * C; i += 512)  // (sum | sum of squares) x channel: token block 0 + block 1
       a.out_stats[(long long)img * 2 * C + i] = spart[i] + spart[2 * C + i];
@@ -921,6 +889,12 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   // Every launch adds exactly 12 to each counter (12 / G per block; G in {2, 4, 6}), so between launches a
   // counter is a multiple of 12 whatever G earlier launches used, and a block's target is the next one.
   // `during` runs between the barriers while lane 0 of wave 0 polls (work that needs no handed-off byte)
+  // Fail loudly: a wait that exhausts its poll bound (a grid that is not co-resident -- another process on
+  // the GPU, a CU mask) would read partial slabs; the block then keeps the counter protocol (every block
+  // still adds, so later launches' targets hold), sets bit 0 of the status word *a.err (the sampler / forward
+  // report ITSD_ERR_HANDOFF) and writes NaN to its output channels (the NaN check of Diffusion.py:100 fires too)
+  __shared__ int hbad;
+  if (tid == 0) hbad = 0;
   auto handoff = [&](int* cnt, auto during) __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -928,9 +902,14 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(cnt, 12 / G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int target = (old / 12 + 1) * 12;
-      for (int it = 0; it < (1 << 22); ++it) {  // bounded: a grid that is not co-resident cannot hang the GPU
-        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      int v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int it = 0; v < target && it < a.spin_bound; ++it) {  // bounded: a grid that is not co-resident cannot hang the GPU
         __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (v < target) {
+        hbad = 1;
+        __hip_atomic_fetch_or(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
@@ -1024,6 +1003,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   // ---- 4. out = x + O Wp^T + bp for this block's output channels; statistics of its channels
   float* const spart = (float*)(sm + R_ST);  // [token block][2][CW]
   bf16_t* out = a.out + (size_t)img * S * C;
+  const float poison = hbad ? __builtin_nanf("") : 0.0f;  // (a failed hand-off: NaN outputs, see handoff)
   for (int cbl = w; cbl < CBg; cbl += 8) {  // (CBg <= 6: one unit a wave, its fragments loaded above)
     const int cb = g * CBg + cbl;
     f32x16 acc[2];
@@ -1038,7 +1018,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
         const int c = 32 * cb + 8 * q + 4 * hh;
         const f32x4 bb = *(const f32x4*)(a.bp + c);
         const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
-        const float v0 = acc[tb][4 * q + 0] + bb[0] + __uint_as_float(rr.x << 16);
+        const float v0 = acc[tb][4 * q + 0] + bb[0] + poison + __uint_as_float(rr.x << 16);
         const float v1 = acc[tb][4 * q + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
         const float v2 = acc[tb][4 * q + 2] + bb[2] + __uint_as_float(rr.y << 16);
         const float v3 = acc[tb][4 * q + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
@@ -1110,6 +1090,7 @@ extern "C" int itsd_debug_stamps_attn(unsigned long long* host) {
 
 int g_attn_wide_nq = 1;  // its query groups a block: 0 auto, 1 / 2 forced (2 measured equal at C3, slower at C4) (itsd_set_option "attn_wide_nq")
 int g_attn_wide = 1;   // channel-split attention: 0 off, 1 auto (C >= 384, S >= 256), 2 wherever attn_cs_ok (itsd_set_option "attn_wide")
+int g_spin_bound = 1 << 22;  // polls before an in-kernel hand-off wait fails (itsd_set_option "spin_bound", diagnostic)
 int g_attn_split = 1;  // attn_block_split_kernel for small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 // G blocks per image for attn_block_split_kernel at batch n (0: one block per image, attn_block_kernel):
 // the largest of 6 / 4 / 2 that keeps the grid co-resident (n * G <= CUs, one block per CU)
@@ -1117,7 +1098,9 @@ int attn_split_g(int n, int C) {
   if (C != 384 || !g_attn_split) return 0;
   const int opts[3] = {6, 4, 2};
   for (int G : opts)
-    if ((g_attn_split == 1 || g_attn_split == G) && (long long)n * G <= g_num_cus) return G;
+    // (co-resident grid: one 512-thread block a CU; the partial-score slab holds 4 MB = 256 x 16 KB)
+    if ((g_attn_split == 1 || g_attn_split == G) && (long long)n * G <= g_num_cus && (long long)n * G * 16384 <= (4ll << 20))
+      return G;
   return 0;
 }
 
@@ -1129,24 +1112,16 @@ hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
     else if (G == 2) ITSD_LAUNCH((attn_block_split_kernel<384, 2>), dim3(a.n * 2), dim3(512), 0, s, a);
     if (G) return hipGetLastError();
   }
-  if (a.S == 16) {  // 4 images a block
-    const dim3 g4((unsigned)((a.n + 3) / 4));
-    if (C == 512) ITSD_LAUNCH((attn_block_kernel<512, 4>), g4, dim3(512), 0, s, a);
-    else if (C == 384) ITSD_LAUNCH((attn_block_kernel<384, 4>), g4, dim3(512), 0, s, a);
-    else if (C == 256) ITSD_LAUNCH((attn_block_kernel<256, 4>), g4, dim3(512), 0, s, a);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
   if (a.S != 64) return hipErrorInvalidValue;
-  if (C == 384) ITSD_LAUNCH((attn_block_kernel<384, 1>), dim3(a.n), dim3(512), 0, s, a);
-  else if (C == 256) ITSD_LAUNCH((attn_block_kernel<256, 1>), dim3(a.n), dim3(512), 0, s, a);
-  else if (C == 128) ITSD_LAUNCH((attn_block_kernel<128, 1>), dim3(a.n), dim3(512), 0, s, a);
+  if (C == 384) ITSD_LAUNCH((attn_block_kernel<384>), dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 256) ITSD_LAUNCH((attn_block_kernel<256>), dim3(a.n), dim3(512), 0, s, a);
+  else if (C == 128) ITSD_LAUNCH((attn_block_kernel<128>), dim3(a.n), dim3(512), 0, s, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 // S = 64: one image a block (LDS: C <= 384); S = 16 (the 4x4 middle block): 4 images a block, C <= 512
 bool attn_block_ok(int S, int C) {
-  return (S == 64 && (C == 128 || C == 256 || C == 384)) || (S == 16 && (C == 256 || C == 384 || C == 512));
+  return S == 64 && (C == 128 || C == 256 || C == 384);
 }
 
 // Flash-style MFMA attention for long sequences (S > 256: the CFG UNet's 32x32 level,
@@ -1819,8 +1794,7 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 // (HBM latency once per batch, not per chunk). Each wave owns 2 x 16 pixels:
 // eps[pixel][co] = sum_k patch[pixel][k] W[co][k] on v_mfma_f32_16x16x32_bf16
 // (k = tap*C + ci; 9C/32 k-steps; B columns 3..15 are zero).
-// TM_PX output pixels per block: 128, or 64 (option "tail_px": a smaller halo, 3 blocks a CU)
-int g_tail_px = 128;
+// TM_PX output pixels per block: 128 (64 -- a smaller halo, 3 blocks a CU -- measured +0.3 %, removed in round 5)
 template <int TM_PX>
 __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   extern __shared__ __attribute__((aligned(16))) char tsm[];
@@ -1991,17 +1965,14 @@ hipError_t launch_tail_mfma(const TailArgs& a, hipStream_t s) {
   if (!a.coef || !a.wmf || !tail_mfma_ok(a.H, a.W, a.C)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)tail_mfma_kernel<128>, (const void*)tail_mfma_kernel<64>}) {
+    for (const void* f : {(const void*)tail_mfma_kernel<128>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
-  if (g_tail_px == 64 && tail_mfma_ok_px(64, a.H, a.W, a.C))
-    ITSD_LAUNCH(tail_mfma_kernel<64>, dim3(a.n * (a.H / (64 / a.W))), dim3(256), tail_mfma_smem_px(64, a.H, a.W, a.C), s, a);
-  else
-    ITSD_LAUNCH(tail_mfma_kernel<128>, dim3(a.n * (a.H / (128 / a.W))), dim3(256), tail_mfma_smem_px(128, a.H, a.W, a.C),
-                s, a);
+  ITSD_LAUNCH(tail_mfma_kernel<128>, dim3(a.n * (a.H / (128 / a.W))), dim3(256), tail_mfma_smem_px(128, a.H, a.W, a.C),
+              s, a);
   return hipGetLastError();
 }
 
@@ -2248,7 +2219,8 @@ __global__ void set_int_kernel(int* p, int v) { *p = v; }
 // the replayed step graph)
 __global__ void run_begin_kernel(int* t, int t_begin, int* nan_flag, RunParams* run, RunParams v) {
   *t = t_begin;
-  *nan_flag = 0;
+  nan_flag[0] = 0;  // the NaN flag (Diffusion.py:100)
+  nan_flag[1] = 0;  // the in-kernel hand-off status word (AttnBlockArgs::err)
   *run = v;
 }
 hipError_t launch_run_begin(int* t, int t_begin, int* nan_flag, RunParams* run, const RunParams& v, hipStream_t s) {

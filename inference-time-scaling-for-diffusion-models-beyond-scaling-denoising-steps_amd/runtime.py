@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # ITSD_LIB: an alternative build of the same library (diagnostic A/B builds under build_diag/)
 LIB_PATH = os.environ.get("ITSD_LIB") or os.path.join(_HERE, "libitsd_hip.so")
 
-ITSD_OK, ITSD_ERR_INVALID, ITSD_ERR_HIP, ITSD_ERR_WEIGHTS, ITSD_ERR_NAN, ITSD_ERR_OOM = range(6)
+ITSD_OK, ITSD_ERR_INVALID, ITSD_ERR_HIP, ITSD_ERR_WEIGHTS, ITSD_ERR_NAN, ITSD_ERR_OOM, ITSD_ERR_HANDOFF = range(7)
 PREC_FP32, PREC_BF16 = 0, 1
 VERIFY_ORACLE, VERIFY_SELFSUP, VERIFY_AESTHETIC, VERIFY_MEAN = 0, 1, 2, 3
 RUN_GRAPH, RUN_CLIP, RUN_SYNC = 1, 2, 4
@@ -72,6 +72,7 @@ _SIGS = {
                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
     "itsd_set_option": [ctypes.c_char_p, ctypes.c_int],
+    "itsd_calibrate": [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p],
     "itsd_unet_query": [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)],
     "itsd_kernel_name": [ctypes.c_int],
     "itsd_last_error": [],
@@ -88,7 +89,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ItsdError(ITSD_ERR_INVALID, f"{LIB_PATH} is not built; run __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
+        shipped = os.path.abspath(LIB_PATH) == os.path.join(_HERE, "libitsd_hip.so")
         for name, args in _SIGS.items():
+            if not shipped and not hasattr(L, name):
+                continue  # (an older build loaded for an A/B measurement: entry points it predates are absent)
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_char_p if name in ("itsd_last_error", "itsd_kernel_name") else ctypes.c_int
@@ -230,7 +234,9 @@ class NativeUNet:
         dec = [decode(int(kinds[i])) for i in range(k)]
         return [{"kind": dec[i][0], "kernel": dec[i][1], "ms": float(ms[i]), "flops": float(fl[i]),
                  "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
-                 "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5]), "op": int(sh[i, 6])} for i in range(k)]
+                 "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5]), "op": int(sh[i, 6]),
+                 "resid": bool(sh[i, 7] & 1), "stats_out": bool(sh[i, 7] & 2), "gn_in": bool(sh[i, 7] & 4)}
+                for i in range(k)]
 
 
 def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset: int = 0,
@@ -240,6 +246,16 @@ def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset
                            int(seed) & ((1 << 64) - 1), int(stream_id) & 0xFFFFFFFF, int(cand_offset),
                            stream_ptr(out.device)))
     return out
+
+
+CALIB_MFMA_BF16, CALIB_HBM_COPY = 0, 1
+
+
+def calibrate(what: int) -> float:
+    """On-box achievable peak: CALIB_MFMA_BF16 -> TFLOP/s, CALIB_HBM_COPY -> GB/s (itsd_calibrate)."""
+    v = ctypes.c_double(0.0)
+    check(lib().itsd_calibrate(int(what), ctypes.byref(v), stream_ptr()))
+    return v.value
 
 
 def set_option(key: str, value: int) -> None:

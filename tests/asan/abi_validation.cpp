@@ -55,20 +55,23 @@ int main() {
   expect("set_option splitk=-1", itsd_set_option("splitk", -1), ITSD_ERR_INVALID);
   expect("set_option small_conv=3", itsd_set_option("small_conv", 3), ITSD_ERR_INVALID);
   expect("set_option gn_wide=7", itsd_set_option("gn_wide", 7), ITSD_ERR_INVALID);
-  expect("set_option gn_reg=5", itsd_set_option("gn_reg", 5), ITSD_ERR_INVALID);
-  expect("set_option gn_reg=4", itsd_set_option("gn_reg", 4), ITSD_OK);
-  expect("set_option gn_reg=3 (removed)", itsd_set_option("gn_reg", 3), ITSD_ERR_INVALID);
-  expect("set_option conv_wide=1 (removed)", itsd_set_option("conv_wide", 1), ITSD_ERR_INVALID);
-  expect("set_option gn_reg=4 (default)", itsd_set_option("gn_reg", 4), ITSD_OK);
+  expect("set_option gn_reg=4 (removed)", itsd_set_option("gn_reg", 4), ITSD_ERR_INVALID);
+  expect("set_option conv_wide=0 (removed)", itsd_set_option("conv_wide", 0), ITSD_ERR_INVALID);
+  expect("set_option p4_m16=1 (removed)", itsd_set_option("p4_m16", 1), ITSD_ERR_INVALID);
+  expect("set_option conv_variant=3 (removed)", itsd_set_option("conv_variant", 3), ITSD_ERR_INVALID);
+  expect("set_option conv_variant=2 (default)", itsd_set_option("conv_variant", 2), ITSD_OK);
+  expect("set_option spin_bound=-1", itsd_set_option("spin_bound", -1), ITSD_ERR_INVALID);
+  expect("set_option spin_bound=4194304 (default)", itsd_set_option("spin_bound", 1 << 22), ITSD_OK);
+  expect("set_option p4_xcd=2", itsd_set_option("p4_xcd", 2), ITSD_ERR_INVALID);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
-  expect("set_option p4_w=16", itsd_set_option("p4_w", 16), ITSD_ERR_INVALID);
+  expect("set_option p4_w=8 (64x64 removed)", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
   expect("set_option convt_prune=2", itsd_set_option("convt_prune", 2), ITSD_ERR_INVALID);
   expect("set_option convt_prune=1 (default)", itsd_set_option("convt_prune", 1), ITSD_OK);
   expect("set_option attn_wide=3", itsd_set_option("attn_wide", 3), ITSD_ERR_INVALID);
-  expect("set_option tail_px=96", itsd_set_option("tail_px", 96), ITSD_ERR_INVALID);
+  expect("set_option tail_px=64 (removed)", itsd_set_option("tail_px", 64), ITSD_ERR_INVALID);
   expect("set_option small_minks=0", itsd_set_option("small_minks", 0), ITSD_ERR_INVALID);
-  expect("set_option attn_fuse=3", itsd_set_option("attn_fuse", 3), ITSD_ERR_INVALID);
-  expect("set_option attn_fuse=2 (default)", itsd_set_option("attn_fuse", 2), ITSD_OK);
+  expect("set_option attn_fuse=2 (removed)", itsd_set_option("attn_fuse", 2), ITSD_ERR_INVALID);
+  expect("set_option attn_fuse=1 (default)", itsd_set_option("attn_fuse", 1), ITSD_OK);
   expect("set_option small_minks=8 (default)", itsd_set_option("small_minks", 8), ITSD_OK);
   expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
   {  // a long key: the error message copies it

@@ -64,3 +64,20 @@ def test_cpu_baseline_conversion_check_fields():
     assert len(c["loop_steps_per_s"]) == 2 and len(c["b1_fwd_per_s"]) == 2
     dev = (max(c["loop_steps_per_s"]) - max(c["b1_fwd_per_s"])) / max(c["b1_fwd_per_s"])
     assert abs(c["deviation"] - dev) < 1e-3 and c["agrees"] == (abs(c["deviation"]) <= 0.15)
+
+
+def test_conv_alg_bytes_counts_every_operand_once():
+    """the algorithmic bytes of a fused conv launch count the residual operand and the
+    GroupNorm statistics slabs (output written, fused input read), besides input, weights and output."""
+    import bench
+    M, N, K = 256 * 1024, 128, 9 * 128
+    o = {"M": M, "N": N, "K": K, "H": 32, "ks": 3, "stride_up": 10, "resid": False, "stats_out": False, "gn_in": False}
+    base = 2.0 * (M * 128 + N * K + M * N)
+    assert bench.conv_alg_bytes(o) == base
+    o.update(resid=True, stats_out=True, gn_in=True)
+    slots = M / 128  # 128-pixel statistics slots of the 32x32 images
+    assert bench.conv_alg_bytes(o) == base + 2.0 * M * N + 8.0 * slots * N + 8.0 * slots * 128
+    # nearest-x2 upsample conv (input grid a quarter of the output's), 4x4 level slots of 16 pixels
+    up = {"M": 4096, "N": 512, "K": 9 * 512, "H": 8, "ks": 3, "stride_up": 11, "resid": False, "stats_out": True,
+          "gn_in": False}
+    assert bench.conv_alg_bytes(up) == 2.0 * (1024 * 512 + 512 * 9 * 512 + 4096 * 512) + 8.0 * (4096 / 64) * 512

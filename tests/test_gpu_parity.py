@@ -337,7 +337,7 @@ def test_channel_split_attention_query_groups_bit_identical(S, C):
     assert _rel_l2(outs[1], _attn_ref(qkv)) < 1e-2
 
 
-_TILE_DEFAULTS = {"gn_wide": 1, "conv_wide": 0, "splitk": 1, "gn_reg": 4, "p4_sub": 1}
+_TILE_DEFAULTS = {"gn_wide": 1, "splitk": 1, "p4_sub": 1}
 
 
 def _eps_with(net, x, t, **opts):
@@ -604,25 +604,6 @@ def test_subpixel_split_k_vs_unsplit(arch, n):
     assert d < 1e-2 and e < REL_L2_BF16  # (measured 5.7e-3 / 7.8e-3: one conv's sum order, through the net)
 
 
-@pytest.mark.parametrize("n", [8, 256])
-def test_tail_64px_blocks_bit_identical(n):
-    """tail_mfma_kernel with 64-pixel blocks (tail_px = 64: a 4-row halo, waves 0-1 run the MFMAs) computes
-    every output exactly as the 128-pixel blocks: sampler steps bit-identical (Philox mode, bf16)."""
-    a = ARCH_A
-    net = _net(a, "bf16")
-    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, a.T)
-    x = torch.randn(n, 3, 32, 32, generator=torch.Generator().manual_seed(700 + n)).cuda()
-
-    def run(px):
-        rt.set_option("tail_px", px)
-        try:
-            return smp.run(x.clone(), t_begin=999, t_end=996, seed=3).cpu()
-        finally:
-            rt.set_option("tail_px", 128)
-
-    assert torch.equal(run(64), run(128))
-
-
 def test_streaming_1x1_convs_vs_conv_pipe_n256():
     """The bench batch's ResBlock shortcuts at 32x32 / 16x16 (K = 256..640) on conv1x1_stream_kernel
     (weights resident in VGPRs, a 4-stage pixel-chunk ring across tiles): the same k order and
@@ -650,143 +631,6 @@ def test_streaming_1x1_convs_vs_conv_pipe_n256():
     with torch.no_grad():
         ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
     assert _rel_l2(st[idx], ref) < REL_L2_BF16
-
-
-def test_p4_64x64_level_vs_p5_c4_batch():
-    """C4's 64x64 level (Arch A at 64 px, N_local = 16: 256 tiles of 4 rows) on conv3x3_gn_p4_kernel<64>
-    (option p4_w bit 3; residual from HBM in the register epilogue, GroupNorm coefficients from
-    gn_coef) against the shipped p5 kernel: the same k order per accumulator, so bit-identical, and
-    within the bf16 bound of the oracle."""
-    a = ARCH_A64
-    net = _net(a, "bf16")
-    n = 16
-    gen = torch.Generator().manual_seed(690)
-    x = torch.randn(n, 3, 64, 64, generator=gen)
-    t = torch.randint(0, a.T, (n,), generator=gen)
-
-    def run(v):
-        rt.set_option("p4_w", v)
-        try:
-            if v & 8:
-                ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
-                assert any("conv3x3_gn_p4_kernel<64>" in o["kernel"] for o in ops if o["H"] == 64)
-            return net(x.cuda(), t.cuda()).float().cpu()
-        finally:
-            rt.set_option("p4_w", 7)
-
-    p4 = run(15)
-    assert torch.equal(p4, run(15))
-    p5 = run(7)
-    idx = [0, n - 1]
-    with torch.no_grad():
-        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
-    d, e = _rel_l2(p4, p5), _rel_l2(p4[idx], ref)
-    print(f"64x64 level: p4 vs p5 rel-L2 {d:.2e}; vs oracle {e:.2e}")
-    assert d == 0.0 and e < REL_L2_BF16
-
-
-@pytest.mark.parametrize("n", [16, 32])
-def test_small_8x8_split_convs_vs_conv_pipe(n):
-    """Small batches: the 8x8 level's plain convs (the 16x16 -> 8x8 DownSample, the shortcuts) whose
-    128x128 conv_pipe grid under-fills the chip run on conv_small's 64x64 whole-image tiles, K split
-    in-launch where a slice keeps >= small_minks K-chunks (shipped 8: these K = 2304 convs run whole, the
-    same k order as conv_pipe; at 2 they split): deterministic, within 1e-2 relative L2 of conv_pipe
-    (small_8x8 = 0), bf16 bound vs oracle."""
-    a = ARCH_A
-    net = _net(a, "bf16")
-    gen = torch.Generator().manual_seed(680 + n)
-    x = torch.randn(n, 3, 32, 32, generator=gen)
-    t = torch.randint(0, a.T, (n,), generator=gen)
-    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
-    assert any(o["kind"] == "conv" and o["H"] == 8 and "conv_small" in o["kernel"] for o in ops)
-
-    def run(v, m=8):
-        rt.set_option("small_8x8", v)
-        rt.set_option("small_minks", m)
-        try:
-            return net(x.cuda(), t.cuda()).float().cpu()
-        finally:
-            rt.set_option("small_8x8", 1)
-            rt.set_option("small_minks", 8)
-
-    w = run(1)
-    assert torch.equal(w, run(1))
-    ws = run(1, 2)
-    assert torch.equal(ws, run(1, 2))
-    p = run(0)
-    idx = [0, n - 1]
-    with torch.no_grad():
-        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
-    d, ds, e = _rel_l2(w, p), _rel_l2(ws, p), _rel_l2(w[idx], ref)
-    print(f"n={n}: 8x8 conv_small vs conv_pipe rel-L2 {d:.2e} (split K {ds:.2e}); vs oracle {e:.2e}")
-    assert d < 1e-2 and ds < 1e-2 and e < REL_L2_BF16
-
-
-@pytest.mark.parametrize("n", [16, 32])
-def test_small_wide_stats_free_convs_vs_conv_pipe(n):
-    """Small batches: the statistics-free convs of 8x8 .. 32x32 images (ResBlock shortcuts, the q|k|v
-    convs) whose 128x128 conv_pipe grid under-fills the chip run on conv_small's 64x64 tiles (inside
-    one image, split K): deterministic, within 1e-2 relative L2 of conv_pipe (small_wide = 0) and
-    within the bf16 bound of the oracle."""
-    a = ARCH_A
-    net = _net(a, "bf16")
-    gen = torch.Generator().manual_seed(660 + n)
-    x = torch.randn(n, 3, 32, 32, generator=gen)
-    t = torch.randint(0, a.T, (n,), generator=gen)
-    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
-    assert any(o["kind"] == "conv" and o["H"] >= 8 and o["ks"] == 1 and "conv_small" in o["kernel"] for o in ops)
-
-    def run(v):
-        rt.set_option("small_wide", v)
-        try:
-            return net(x.cuda(), t.cuda()).float().cpu()
-        finally:
-            rt.set_option("small_wide", 1)
-
-    w = run(1)
-    assert torch.equal(w, run(1))
-    p = run(0)
-    idx = [0, n - 1]
-    with torch.no_grad():
-        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
-    d, e = _rel_l2(w, p), _rel_l2(w[idx], ref)
-    print(f"n={n}: conv_small (wide) vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
-    assert d < 1e-2 and e < REL_L2_BF16
-
-
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_dead_tap_pruning_archC_1x1_level(precision):
-    """Arch C's 1x1 level (ModelCondition.py: ch_mult [1, 4, 8, 8, 4, 2] at 32 px): taps that read only
-    padding for every output pixel are dropped at build time -- the 3x3 convs on 1x1 images run their
-    centre tap (ks 1), the DownSample 2x2 -> 1x1 (c1 3x3 + c2 5x5, stride 2, merged into one 5x5 conv at
-    build time) a 2x2 window, the ConvTranspose
-    from the 1x1 grid its centre tap per phase. Exact in arithmetic (the dropped taps multiply zero
-    padding): the census shows no 3x3+ conv left at H = 1, and a guided batch (2N = 64, the C3 leg's)
-    matches the oracle (fp32 max|d| <= 2e-4, bf16 rel-L2 <= 2e-2)."""
-    a = ARCH_C
-    net = _net(a, precision)
-    n = 64
-    gen = torch.Generator().manual_seed(641)
-    xc = torch.randn(n, 3, 32, 32, generator=gen)
-    tc = torch.randint(0, a.T, (n,), generator=gen)
-    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n // 2, dtype=torch.long)])
-    x, t, lb = xc.cuda(), tc.cuda(), lab.cuda()
-    ops = net.native(n).profile_ops(x, t.to(torch.int32))
-    h1 = [o for o in ops if o["kind"] == "conv" and o["H"] == 1]
-    assert h1 and all(o["ks"] <= 2 for o in h1), [(o["ks"], o["K"], o["kernel"]) for o in h1]
-    assert sum(o["ks"] == 2 for o in h1) == 1  # the DownSample into the 1x1 level (c1 + c2 as one 5x5 s2 conv)
-    eps = net(x, t, lb).float().cpu()
-    idx = [0, 31, 32, n - 1]
-    with torch.no_grad():
-        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
-    if precision == "fp32":
-        d = (eps[idx] - ref).abs().max().item()
-        print(f"Arch C 2N=64 fp32 (pruned taps) max|d| vs oracle {d:.2e}")
-        assert d <= EPS_TOL_FP32
-    else:
-        e = _rel_l2(eps[idx], ref)
-        print(f"Arch C 2N=64 bf16 (pruned taps, LDS-staged flash attention) rel-L2 vs oracle {e:.2e}")
-        assert e < REL_L2_BF16
 
 
 def test_forward_bf16_full_batch_vs_oracle_subset():

@@ -86,11 +86,18 @@ def test_conv_tile_options():
         with pytest.raises(rt.ItsdError):
             rt.set_option(key, 3)
         rt.set_option(key, default)
-    rt.set_option("conv_wide", 0)
-    rt.set_option("gn_reg", 4)
-    for key, val in (("conv_wide", 1), ("gn_reg", 0), ("gn_reg", 3)):  # removed generations (round 4)
-        with pytest.raises(rt.ItsdError, match="removed|only 4"):
+    # measured-and-dropped paths (removed in rounds 4-5): their switches are unknown keys or refused values
+    for key, val in (("conv_wide", 0), ("gn_reg", 4), ("tail_px", 64), ("p4_m16", 1), ("small_korder", 1)):
+        with pytest.raises(rt.ItsdError, match="unknown option"):
             rt.set_option(key, val)
+    for key, val, default in (("attn_fuse", 2, 1), ("p4_w", 15, 7), ("conv_variant", 3, 2), ("conv_variant", 0, 2)):
+        with pytest.raises(rt.ItsdError):
+            rt.set_option(key, val)
+        rt.set_option(key, default)
+    rt.set_option("spin_bound", 0)  # diagnostic (fail-loud hand-off test), any bound >= 0
+    rt.set_option("spin_bound", 1 << 22)
+    with pytest.raises(rt.ItsdError):
+        rt.set_option("spin_bound", -1)
     rt.set_option("conv_dbg", 1)
     with pytest.raises(rt.ItsdError, match="diagnostic builds only"):
         rt.set_option("conv_dbg", 4096 | (2 << 13))
@@ -109,6 +116,9 @@ def test_shipped_library_holds_only_product_kernels():
         __graft_entry__.build()
     blob = open(rt.LIB_PATH, "rb").read()
     for name in (b"conv3x3_gn_wide_kernel", b"conv3x3_gn_reg_kernel", b"conv3x3_gn_ws_kernel",
-                 b"conv3x3_gn_pws_kernel", b"conv_pipe_wide", b"itsd_debug_stamps"):
+                 b"conv3x3_gn_pws_kernel", b"conv_pipe_wide", b"itsd_debug_stamps",
+                 # round 5: the dropped 16x16x32 p4 form, p4 at 64x64, the 4-image AttnBlock, 3/4-stage pipes
+                 b"conv3x3_gn_p4_kernelILi32ELi0ELb1", b"conv3x3_gn_p4_kernelILi64", b"attn_block_kernelILi512ELi4",
+                 b"conv_pipeItLi3", b"conv_pipeItLi4", b"tail_mfma_kernelILi64"):
         assert name not in blob, name
     assert b"conv3x3_gn_p4_kernel" in blob

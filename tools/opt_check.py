@@ -1,7 +1,7 @@
 """eps of one bf16 Arch A forward under itsd_set_option overrides vs the defaults (relative L2),
 plus the oracle-free determinism check (two runs of each variant bit-identical).
 
-    python tools/opt_check.py --n 8,256 small_raw=0 gn_reg=3
+    python tools/opt_check.py --n 8,256 small_conv=0 p4_w=3
 """
 import argparse
 import os
@@ -38,7 +38,7 @@ def main():
             rel = ((e1 - base).norm() / base.norm()).item()
             print(f"n={n} {v}: rel-L2 vs default {rel:.3e}, deterministic {torch.equal(e1, e2)}", flush=True)
             for k, val in kv:
-                rt.set_option(k, {"small_korder": 0, "conv_dbg": 0, "gn_reg": 4, "p4_w": 7, "small_conv": 1, "p4_m16": 0, "attn_aq": 0, "attn_cs": 0}[k])
+                rt.set_option(k, {"conv_dbg": 0, "p4_w": 7, "small_conv": 1, "attn_aq": 0, "attn_cs": 0}[k])
 
 
 if __name__ == "__main__":

@@ -3,13 +3,8 @@ hipcc -DITSD_STAMPS, see conv.hip; per wave, s_memtime cycles). Never part of th
 
     python tools/stamps.py build_diag/libitsd_hip_stamps.so [op_index ...]
 
-ITSD_GN_REG selects the kernel (itsd_set_option "gn_reg"):
-  0 -> conv3x3_gn_wide_kernel: wait / barrier / weight-DMA issue / MFMA issue / GN transform,
-       prologue, epilogue, total (8 waves);
-  3 -> conv3x3_gn_pws_kernel (persistent): MFMA waves 0..7, halo waves 8..11;
-  4 -> conv3x3_gn_p4_kernel (persistent, one MFMA wave per SIMD): MFMA waves 0..3, halo 4..7;
-  2 -> conv3x3_gn_ws_kernel: MFMA waves 0..7 (chunk compute, barrier wait, prologue, epilogue,
-       total) and halo waves 8..11 (halo staging, barrier wait, chunk-0 staging, output pass, total).
+conv3x3_gn_p4_kernel (persistent, one MFMA wave per SIMD): MFMA waves 0..3 (chunk compute, barrier
+wait, epilogue, total), halo waves 4..7 (stage transform, barrier wait, prologue, total).
 """
 import ctypes
 import os
@@ -27,16 +22,16 @@ from itsd.arch import ARCH_A
 from itsd.model import UNet
 
 N = int(os.environ.get("ITSD_N", "256"))
-GN_REG = int(os.environ.get("ITSD_GN_REG", "3"))
+GN_REG = 4  # (the superseded generations 0-3 and their "gn_reg" switch are gone)
 a = ARCH_A
 net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, precision="bf16", weights="gauss").to("cuda:0")
 nat = net.native(N)
 x = torch.randn(N, 3, 32, 32, device="cuda")
 t = torch.full((N,), 500, dtype=torch.int32, device="cuda")
 L = rt.lib()
-L.itsd_set_option(b"gn_reg", GN_REG)
 ops = nat.profile_ops(x, t)
-sel = [int(v) for v in sys.argv[2:]] or [i for i, o in enumerate(ops) if o["kind"] in ("convgnw", "convgnw4")][:6]
+conv_p4 = [i for i, o in enumerate(ops) if o["kind"] in ("convgnw", "convgnw4")]
+sel = conv_p4 if sys.argv[2:] == ["all"] else ([int(v) for v in sys.argv[2:]] or conv_p4[:6])
 for i in sel:
     o = ops[i]
     L.itsd_set_option(b"conv_dbg", int(os.environ.get("ITSD_DBG", "0")))

@@ -21,8 +21,8 @@ from itsd.model import UNet
 # the shipped value of every option a variant may touch (a variant's keys are reset to these after it runs)
 DEFAULTS = {"gn_fold": 1, "p5": 1, "p5_split": 0, "splitk_inl": 1, "p4_plain": 1, "splitk": 1, "attn_split": 1,
             "p4_sub": 1, "gn_wide": 1, "small_conv": 1, "conv_variant": 2, "small_wide": 1, "small_8x8": 1,
-            "subpix_split": 1, "conv1x1": 1, "tail_px": 128, "attn_wide": 1, "attn_wide_nq": 1, "p4_w": 7, "convt_prune": 1, "small_minks": 8,
-            "attn_fuse": 2, "fuse_gn": 1, "conv_dbg": 0, "small_korder": 0}
+            "subpix_split": 1, "conv1x1": 1, "attn_wide": 1, "attn_wide_nq": 1, "p4_w": 7, "convt_prune": 1, "small_minks": 8,
+            "attn_fuse": 1, "fuse_gn": 1, "conv_dbg": 0, "p4_xcd": 0, "spin_bound": 1 << 22}
 
 
 def main():
@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="base")
-    ap.add_argument("--create-set", default="", help="options set before the UNet is created, e.g. attn_fuse=2")
+    ap.add_argument("--create-set", default="", help="options set before the UNet is created, e.g. attn_fuse=0")
     ap.add_argument("--lib", default="", help="another build of libitsd_hip.so (A/B of two builds in two processes)")
     args = ap.parse_args()
     if args.lib:
