@@ -51,11 +51,19 @@ __global__ __launch_bounds__(256, 2) void calib_mfma_kernel(float* out, int iter
   out[gid] = s;
 }
 
-// HBM streaming copy: 16 B a lane loads and stores, grid-stride (MI355X_MICROARCH.md: float4 copy
-// measured 6.29 TB/s of the 8 TB/s spec); bytes counted = read + written
+// HBM streaming copy: 16 B a lane loads and stores, 4 independent loads in flight per lane before their
+// stores (a grid-stride loop of single loads leaves each wave one load deep), nontemporal stores
+// (MI355X_MICROARCH.md: float4 copy measured 6.29 TB/s of the 8 TB/s spec); bytes counted = read + written.
+// n is a multiple of 4 * gridDim.x * blockDim.x (the host sizes it so).
 __global__ __launch_bounds__(256) void calib_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, long long n) {
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
 }
 
 // what: ITSD_CALIB_MFMA_BF16 -> TFLOP/s, ITSD_CALIB_HBM_COPY -> GB/s (read + written); synchronous on s.
@@ -90,7 +98,8 @@ int calibrate_run(int what, double* value, hipStream_t s) {
     if (!rc && hipMemsetAsync(src, 1, bytes, s) != hipSuccess) rc = ITSD_ERR_HIP;
     for (int r = 0; r < 4 && !rc; ++r) {
       hipEventRecord(e0, s);
-      hipLaunchKernelGGL(calib_copy_kernel, dim3(cus * 16), dim3(256), 0, s, (const u32x4*)src, (u32x4*)dst, bytes / 16);
+      // (1 GiB / 16 B = 2^26 units, a multiple of 4 x the 2^12 blocks x 256 threads: every index in range)
+      hipLaunchKernelGGL(calib_copy_kernel, dim3(4096), dim3(256), 0, s, (const u32x4*)src, (u32x4*)dst, bytes / 16);
       hipEventRecord(e1, s);
       if (hipEventSynchronize(e1) != hipSuccess) { rc = ITSD_ERR_HIP; break; }
       float ms = 0.0f;

@@ -1462,6 +1462,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
   // (sub-pixel forms: 4 slots, dividing every phase's k-step count: 16, or 36 / 24 / 24 / 16 live)
+  // (diagnostic AB bits: 64 a 4-slot A ring, 32 three B buffers; round 5 also measured the B reads in a step's first
+  // four MFMA gaps and a 9-slot A ring: +1.5 / -0.7 %, both spilling, profiles/r05/p4_sched_variants.txt)
   constexpr int RING = ((AB & 64) || SUB) ? 4 : P4_RING, BD = (AB & 32) ? P4_BD + 1 : P4_BD;
   static_assert(KST % RING == 0, "ring slots repeat per chunk");
   // + gn_fold: per halo wave, the group mean / rstd of the image it stages [32 groups][2]

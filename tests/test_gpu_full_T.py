@@ -134,6 +134,50 @@ def test_C2_bf16_round_T1000_candidates_and_scores_vs_oracle(full_T):
         assert ds <= FULL_T_BF16_SCORE
 
 
+C5_T, C5_N, C5_CANDS, C5_SEED = 3000, 128, (0, 64, 127), 33
+STREAM_PERTURB = 0xE0000000  # itsd.search._STREAM_PERTURB: perturbed candidates (pivot + scale z) of round 0
+
+
+def test_C5_path_search_round_T3000_candidates_and_scores_vs_oracle():
+    """C5 at full length (VERDICT r4 #5a): one bf16 path-search round (``search/search_algorithm.py:265-336``;
+    candidates = pivot + 0.1 z) of the bench shard N = 128 over the whole T = 3000 schedule of
+    ``fine_tune_extended_T.py`` (betas 1e-4 .. 0.02), three candidates (0, 64, 127) -- the denoised x0 and the
+    OracleVerifier score the search prunes on -- against the oracle's full 3000-step fp32 loop on the same
+    x_T and Philox noise. Bounds: C5_BF16_REL_L2 / C5_BF16_SCORE, derived (tests/golden/tolerance_derivation.json)."""
+    a = dataclasses.replace(ARCH_A, T=C5_T)
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
+    net.load_state_dict(synthetic_state_dict(a, 0))
+    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, C5_T)
+    eng = SearchEngine(smp, OracleVerifier(), seed=C5_SEED)
+    shape = (1, 3, 32, 32)
+    pivot = eng.initial_noise(shape)
+    r = eng.run_round(0, C5_N, shape, pivot=pivot, scale=0.1, kind="path")
+    run_seed = (C5_SEED * 1000003 + 0) & ((1 << 62) - 1)
+    # the candidates' x_T regenerated on the device (the same kernel, bit-identical) -> the oracle's start
+    x_T = torch.cat([eng.candidate_noise(0, i, 1, shape, pivot=pivot, scale=0.1) for i in C5_CANDS]).cpu()
+    x0 = r.local_images.cpu()
+    scores = r.scores.clone()
+    del eng, smp, net
+    torch.cuda.empty_cache()
+    streams = [(run_seed, i * PER) for i in C5_CANDS]
+
+    def noise(step, xx):
+        return torch.stack([R.philox_normal(sd_, step, np.arange(o, o + PER)).reshape(3, 32, 32) for sd_, o in streams])
+
+    sd = synthetic_state_dict(a, 0)
+    fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
+    with torch.no_grad():
+        ref = R.p_sample_loop(fw, x_T, R.schedule(1e-4, 0.02, C5_T), noise)
+    for k, i in enumerate(C5_CANDS):
+        rel = _rel_l2(x0[i], ref[k])
+        s_ref = R.oracle_score(ref[k:k + 1])
+        ds = abs(float(scores[i]) - s_ref)
+        print(f"C5 bf16 path candidate {i}: T=3000 x0 rel-L2 {rel:.3e}, max|d| {(x0[i] - ref[k]).abs().max().item():.3e}; "
+              f"score {float(scores[i]):.6f} vs oracle {s_ref:.6f} (|d| {ds:.2e})")
+        assert rel <= C5_BF16_REL_L2
+        assert ds <= C5_BF16_SCORE
+
+
 def test_C1c_main_condition_eval_T1000_fp32_vs_oracle(tmp_path):
     """MainCondition.py's eval (``TrainCondition.py:118-151`` through ``itsd.entry`` with
     config/condition_config.yaml keys): the class-block labels of batch_size 10, guided sampling
