@@ -1453,14 +1453,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr bool SUB = (AB & 128) != 0, PLAIN = SUB || (AB & 2) != 0;
   constexpr bool SUB4 = SUB && (AB & 256) == 0;      // upsample phases: 2x2 taps; else 3x3 windows
   constexpr int NTAP = SUB4 ? 4 : 9, KST = 4 * NTAP;  // taps and 16-deep k-steps of a 64-channel chunk
-  constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = GnpCfg<W>::ITEMS, RES = GnpCfg<W>::RES;
+  // COMPACT (round 5; tiles of whole images: the 16x16 level's one image, the 8x8 level's four, non-sub-pixel
+  // forms): the halo holds only the tile's 256 interior pixels, row = tile pixel, plus one zero row that every
+  // tap reading outside its image is pointed at -- 256 rows staged a stage instead of 324 / 400 (the padding
+  // frame is never loaded, transformed or written), 33 KB a buffer instead of 44 / 53 KB, so the 8x8 level
+  // has room for the LDS residual / output tile (RES) and its halo-wave drain instead of the register epilogue
+  constexpr bool COMPACT = !SUB && (W == 8 || W == 16);
+  constexpr int NSEG = GnpCfg<W>::NSEG, ITEMS = COMPACT ? 8 : GnpCfg<W>::ITEMS, RES = COMPACT ? 1 : GnpCfg<W>::RES;
   constexpr int W2 = W + 2;
   constexpr int THs = NSEG == 1 ? GNW_BN / W : W;
   constexpr int HS = (THs + 2) * W2;
+  constexpr int HWs = THs * W;  // pixels of one image segment
   constexpr int TPS = 256 / NSEG, RPP = TPS / 8;
-  constexpr int HALO = NSEG * ITEMS * RPP * ROWB;
+  constexpr int ZROW = GNW_BN;  // COMPACT: the zero row
+  constexpr int HALO = COMPACT ? (((GNW_BN + 1) * ROWB + 1023) & ~1023) : NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
-  static_assert(ITEMS * RPP >= HS, "halo items cover the segment");
+  static_assert(COMPACT ? ITEMS * RPP == HWs : ITEMS * RPP >= HS, "halo items cover the segment");
   // (sub-pixel forms: 4 slots, dividing every phase's k-step count: 16, or 36 / 24 / 24 / 16 live)
   // (diagnostic AB bits: 64 a 4-slot A ring, 32 three B buffers; round 5 also measured the B reads in a step's first
   // four MFMA gaps and a 9-slot A ring: +1.5 / -0.7 %, both spilling, profiles/r05/p4_sched_variants.txt)
@@ -1565,12 +1573,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     // wave w: couts 64*(w & 1) .. +63 (two 32-cout A fragments per k-step), pixels 128*(w >> 1) ..
     // +127 (four B fragments): 8 MFMAs per k-step on 128 accumulator registers (AGPRs)
     const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
-    int hb[4];
+    int hb[4];  // halo row of this lane's pixel at tap (0, 0) (COMPACT: the tile pixel itself)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pl = wn * 128 + j * 32 + rl;
       const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
-      hb[j] = seg * HS + oy * W2 + (rem - oy * W);
+      hb[j] = COMPACT ? pl : seg * HS + oy * W2 + (rem - oy * W);
     }
     const uint32_t ablk = (uint32_t)(NTAP * kpt) * 1024;  // one 32-cout block of fragments
     // A fragments by buffer loads: resource = the whole wfrag array, voffset = this lane's 16 B of the wave's
@@ -1622,11 +1630,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 ad = *(const f32x4*)(addv + (kk & 1) * CONV_BM + (2 * wm + i) * 32 + 8 * g + 4 * hh);
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 4; ++j) {
+            // (the image segment of pixel block j: NSEG = 4 -- 64-pixel images -- has two a wave)
+            const int seg = NSEG == 1 ? 0 : (wn * 128 + j * 32) / HWs;
+            const f32x4 ad = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * CONV_BM + (2 * wm + i) * 32 + 8 * g + 4 * hh);
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = ad[e];
+          }
         }
     };
     stage_addv(0, tid);  // (off the halo waves' stage-0 critical path)
@@ -1684,8 +1695,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
           if (kk == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              int h = hb[j] + ky * W2 + kx;
-              asm volatile("" : "+v"(h));
+              int h;
+              if constexpr (COMPACT) {  // the tap's pixel inside the image, else the zero row
+                int p = hb[j];
+                asm volatile("" : "+v"(p));
+                const int x = (p & (W - 1)) + kx - 1, y = ((p / W) & (W - 1)) + ky - 1;
+                h = ((unsigned)x < (unsigned)W && (unsigned)y < (unsigned)W) ? p + (ky - 1) * W + (kx - 1) : ZROW;
+              } else {
+                h = hb[j] + ky * W2 + kx;
+                asm volatile("" : "+v"(h));
+              }
               tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
             }
           }
@@ -1915,11 +1934,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // segments for scratch rows) and a mask that zeroes padding rows (rewritten every stage: the
   // padding rows differ between tiles). Stage and tile indices advance by counters (no divides).
   const int tt = tid - 256, lch = tt & 7, sg = tt / TPS, lt = tt - sg * TPS;
-  static_assert(NSEG * ITEMS * RPP > NSEG * HS, "a scratch row exists");
+  static_assert(COMPACT || NSEG * ITEMS * RPP > NSEG * HS, "a scratch row exists");
   if (a.dbg & (1 << 20)) __builtin_amdgcn_s_setprio(1);  // measurement switches, as in the ws kernel
   if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
-  const int dump = NSEG * HS * ROWB + (lch << 4);
-  const int hrow0 = sg * HS + (lt >> 3), hrow1 = hrow0 + RPP;
+  const int dump = NSEG * HS * ROWB + (lch << 4);  // (not COMPACT: the scratch rows' write target)
+  const int hrow0 = (COMPACT ? sg * HWs : sg * HS) + (lt >> 3), hrow1 = hrow0 + RPP;
   const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
   const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
   auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
@@ -1985,17 +2004,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const int r = (ltv >> 3) + RPP * j;
-      const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
-      const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
+      if constexpr (COMPACT) {  // every item an interior pixel of image img0 + sg
+        ipix[j] = (img0 + sg) * HWs + r;
+      } else {
+        const int hy = r / W2, hx = r - hy * W2, iy = y0 + hy - 1, ix = hx - 1;
+        const bool ok = r < HS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        ipix[j] = ok ? ((img0 + sg) * H + iy) * W + ix : 0;
+      }
     }
     if constexpr (!PLAIN) cbase = a.gn_coef + ((size_t)(img0 + sg) * (Cin / 8) + lch) * 16;
     simg = img0 + sg;
   };
   // Only the last item can hold scratch rows (ITEMS * RPP - HS < RPP for every W): its write
   // address is chosen once; the other items' addresses are lds0/lds1 plus constants.
-  static_assert(ITEMS * RPP - HS < RPP, "scratch rows only in the last item");
-  const int waddr_last = ((lt >> 3) + RPP * (ITEMS - 1)) < HS ? item_lds(ITEMS - 1) : dump;
+  static_assert(COMPACT || ITEMS * RPP - HS < RPP, "scratch rows only in the last item");
+  const int waddr_last = (COMPACT || ((lt >> 3) + RPP * (ITEMS - 1)) < HS) ? item_lds(ITEMS - 1) : dump;
   auto waddr = [&](int j) { return j == ITEMS - 1 ? waddr_last : item_lds(j); };
   int inm = 0;  // bit j: item j's row is real input (or scratch) -- else zero padding
   auto geometry_emit = [&](int k) __attribute__((always_inline)) {
@@ -2004,6 +2027,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     int ltv = lt;
     asm volatile("" : "+v"(ltv));
     inm = 0;
+    if constexpr (COMPACT) {
+      inm = (1 << ITEMS) - 1;  // (no padding rows)
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const int r = (ltv >> 3) + RPP * j;
@@ -2061,53 +2088,58 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       int lane = tid & 63;
       asm volatile("" : "+v"(lane));
       const int tileP = tile_p(kd), tileC = tile_c(kd), u = lane & 7, dph = tile_ph(kd);
-      float v[16];
+      // statistics slots: 128 pixels (one a wave half), or 64 at the 8x8 level (COMPACT RES: two a wave half)
+      constexpr int NH = NSEG == 4 ? 2 : 1;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = 0.f;
+      for (int hf = 0; hf < NH; ++hf) {
+        float v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 128 * ds + 8 * i + (lane >> 3);
-        const u32x4 d = *(const u32x4*)(rlds + dh * 32768 + row * 128 + ((u ^ ((row >> 1) & 7)) << 4));
-        *(u32x4*)((T*)a.out + orow(tileP + row, dph) * a.Cout + tileC + dh * 64 + u * 8) = d;
+        for (int e = 0; e < 16; ++e) v[e] = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const float lo = __uint_as_float(d[w] << 16), hi = __uint_as_float(d[w] & 0xffff0000u);
-          v[2 * w] += lo;
-          v[2 * w + 1] += hi;
-          v[8 + 2 * w] = fmaf(lo, lo, v[8 + 2 * w]);
-          v[8 + 2 * w + 1] = fmaf(hi, hi, v[8 + 2 * w + 1]);
-        }
-      }
-      if (a.stats) {
-        auto xchg = [&](float x, auto wc) {
-          constexpr int w = decltype(wc)::value;
-          const int xi = __builtin_bit_cast(int, x);
-          int r;
-          if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);  // row_ror:8
-          else if constexpr (w == 16) r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (16 << 10));
-          else r = __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, xi);
-          return __builtin_bit_cast(float, r);
-        };
-        auto halve = [&](auto wc, int n) {
-          const bool up = (lane & decltype(wc)::value) != 0;
+        for (int i = hf * 16 / NH; i < (hf + 1) * 16 / NH; ++i) {
+          const int row = 128 * ds + 8 * i + (lane >> 3);
+          const u32x4 d = *(const u32x4*)(rlds + dh * 32768 + row * 128 + ((u ^ ((row >> 1) & 7)) << 4));
+          *(u32x4*)((T*)a.out + orow(tileP + row, dph) * a.Cout + tileC + dh * 64 + u * 8) = d;
 #pragma unroll
-          for (int ii = 0; ii < 8; ++ii) {
-            if (ii < n) {
-              const float lo = v[ii], hi = v[ii + n];
-              v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
-            }
+          for (int w = 0; w < 4; ++w) {
+            const float lo = __uint_as_float(d[w] << 16), hi = __uint_as_float(d[w] & 0xffff0000u);
+            v[2 * w] += lo;
+            v[2 * w + 1] += hi;
+            v[8 + 2 * w] = fmaf(lo, lo, v[8 + 2 * w]);
+            v[8 + 2 * w + 1] = fmaf(hi, hi, v[8 + 2 * w + 1]);
           }
-        };
-        halve(std::integral_constant<int, 8>{}, 8);
-        halve(std::integral_constant<int, 16>{}, 4);
-        halve(std::integral_constant<int, 32>{}, 2);
-        long long slot = (long long)tileP / 128 + ds;
-        if constexpr (SUB) {  // (image, phase, 128-pixel slot of the phase image): the 2x grid has 4x the slots
-          const int HWi = H * W, spp = HWi / 128, img = tileP / HWi;
-          slot = (long long)img * 4 * spp + dph * spp + (tileP - img * HWi) / 128 + ds;
         }
-        const int co = dh * 64 + 8 * u + 4 * ((lane >> 4) & 1) + 2 * (lane >> 5);
-        *(float2*)(a.stats + (slot * 2 + ((lane >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
+        if (a.stats) {
+          auto xchg = [&](float x, auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const int xi = __builtin_bit_cast(int, x);
+            int r;
+            if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);  // row_ror:8
+            else if constexpr (w == 16) r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (16 << 10));
+            else r = __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, xi);
+            return __builtin_bit_cast(float, r);
+          };
+          auto halve = [&](auto wc, int n) {
+            const bool up = (lane & decltype(wc)::value) != 0;
+#pragma unroll
+            for (int ii = 0; ii < 8; ++ii) {
+              if (ii < n) {
+                const float lo = v[ii], hi = v[ii + n];
+                v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+              }
+            }
+          };
+          halve(std::integral_constant<int, 8>{}, 8);
+          halve(std::integral_constant<int, 16>{}, 4);
+          halve(std::integral_constant<int, 32>{}, 2);
+          long long slot = NH == 1 ? (long long)tileP / 128 + ds : ((long long)tileP + 128 * ds + 64 * hf) / 64;
+          if constexpr (SUB) {  // (image, phase, 128-pixel slot of the phase image): the 2x grid has 4x the slots
+            const int HWi = H * W, spp = HWi / 128, img = tileP / HWi;
+            slot = (long long)img * 4 * spp + dph * spp + (tileP - img * HWi) / 128 + ds;
+          }
+          const int co = dh * 64 + 8 * u + 4 * ((lane >> 4) & 1) + 2 * (lane >> 5);
+          *(float2*)(a.stats + (slot * 2 + ((lane >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
+        }
       }
     }
   };
@@ -2207,6 +2239,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     if (a.gn_fold) group_stats(simg);  // (its loads in flight with stage 0's)
     gimg = simg;
     prescale();
+  }
+  if constexpr (COMPACT) {  // the zero row of both halo buffers (no stage writes it; read after B0)
+    if (tt < 16) *(u32x4*)(smem + (tt >> 3) * HALO + ZROW * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
   }
   emit(smem);
 #ifdef ITSD_STAMPS

@@ -48,6 +48,14 @@ static itsd_unet_desc arch_a() {
 int main() {
   expect("itsd_version", itsd_version() >= 1 ? ITSD_OK : 1, ITSD_OK);
 
+  // ---- itsd_calibrate: argument checks (no device here: a valid request fails in HIP)
+  {
+    double v = 0.0;
+    expect("calibrate null value", itsd_calibrate(ITSD_CALIB_MFMA_BF16, nullptr, nullptr), ITSD_ERR_INVALID);
+    expect("calibrate what=7", itsd_calibrate(7, &v, nullptr), ITSD_ERR_INVALID);
+    expect("calibrate mfma, no GPU", itsd_calibrate(ITSD_CALIB_MFMA_BF16, &v, nullptr), ITSD_ERR_HIP);
+  }
+
   // ---- itsd_set_option: null / unknown key, out-of-range values, valid values restored
   expect("set_option null key", itsd_set_option(nullptr, 0), ITSD_ERR_INVALID);
   expect("set_option unknown key", itsd_set_option("no_such_option", 1), ITSD_ERR_INVALID);

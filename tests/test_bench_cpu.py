@@ -63,7 +63,9 @@ def test_cpu_baseline_conversion_check_fields():
     assert r["kind"] == "port" and r["cores"] >= 1 and r["value"] > 0
     assert len(c["loop_steps_per_s"]) == 2 and len(c["b1_fwd_per_s"]) == 2
     dev = (max(c["loop_steps_per_s"]) - max(c["b1_fwd_per_s"])) / max(c["b1_fwd_per_s"])
-    assert abs(c["deviation"] - dev) < 1e-3 and c["agrees"] == (abs(c["deviation"]) <= 0.15)
+    # (the rates in the record are rounded to 3 decimals: at a few steps/s on a loaded host that alone moves
+    # the recomputed deviation by ~1e-3)
+    assert abs(c["deviation"] - dev) < 5e-3 and c["agrees"] == (abs(c["deviation"]) <= 0.15)
 
 
 def test_conv_alg_bytes_counts_every_operand_once():
