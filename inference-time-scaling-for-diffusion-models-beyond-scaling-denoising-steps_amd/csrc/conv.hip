@@ -2470,7 +2470,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           if (pf < 36) load_a(cb, pf, ra[pf % P5_RING]);
           else load_a(nb, pf - 36, ra[pf % P5_RING]);
           if (step + P5_BD - 1 < 36) rd(step + P5_BD - 1, (step + P5_BD - 1) % P5_BD);
-          __builtin_amdgcn_sched_barrier(0);
           const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % P5_RING]);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -2479,6 +2478,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             else
 #endif
             acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc[j], 0, 0, 0);
+          // (round 5) the step's A load, B reads and address VALU spread over its 4 MFMA gaps, as in
+          // conv3x3_gn_p4_kernel, instead of all of them ahead of the MFMAs: the tap-boundary address
+          // rebuilds no longer stall the matrix pipe
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (q == 0) TL(6);

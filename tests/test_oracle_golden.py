@@ -170,3 +170,25 @@ def test_verifier_branches():
     for case in ("p32", "p64"):
         got = R.selfsup_paired_score(torch.from_numpy(g[case + "_images"]), torch.from_numpy(g[case + "_ref"]))
         assert abs(got - float(g[case + "_paired"])) <= 1e-7
+
+
+def test_full_T_tolerances_follow_from_the_recorded_drifts():
+    """The full-length GPU parity bounds (tests/test_gpu_full_T.py) are derived, not tuned: each equals its
+    factor times a drift of the oracle's own loop recorded by tools/derive_tolerances.py (fp32: 4 x 2 x the
+    fp32-vs-fp64 drift of the saved image; bf16: 2 x the bf16 emulation's drift), and the bf16 emulation's
+    drift at T = 1000 is of the size the GPU's bf16 path shows against the fp32 oracle (round 4: x0 rel-L2
+    3.0-3.4e-2), i.e. the emulation models the GPU's rounding."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "tolerance_derivation.json")) as fh:
+        d = json.load(fh)
+    t, f32, f16 = d["tolerances"], d["factor_fp32"], d["factor_bf16"]
+    assert d["T"] == 1000 and d["C5_bf16_emulation"]["T"] == 3000
+    assert t["FULL_T_FP32_MAXABS"] == f32 * 2 * d["C1_archA_fp32_vs_fp64"]["image_maxabs"]
+    assert t["FULL_T_FP32_CFG_MAXABS"] == f32 * 2 * d["C1c_cfg_fp32_vs_fp64"]["image_maxabs"]
+    assert t["FULL_T_BF16_REL_L2"] == f16 * d["C2_bf16_emulation"]["x0_rel_l2_max"]
+    assert t["FULL_T_BF16_SCORE"] == f16 * d["C2_bf16_emulation"]["score_absdiff_max"]
+    assert t["C5_BF16_REL_L2"] == f16 * d["C5_bf16_emulation"]["x0_rel_l2_max"]
+    assert t["C5_BF16_SCORE"] == f16 * d["C5_bf16_emulation"]["score_absdiff_max"]
+    assert 1e-2 < d["C2_bf16_emulation"]["x0_rel_l2_max"] < 5e-2
+    assert d["C1_archA_fp32_vs_fp64"]["image_maxabs"] < 1e-4 < d["C2_bf16_emulation"]["x0_rel_l2_max"]
