@@ -448,10 +448,13 @@ def main():
             from itsd import runtime as rt
             progress("calibration: bf16 MFMA loop, HBM copy")
             mf, hb = rt.calibrate(rt.CALIB_MFMA_BF16), rt.calibrate(rt.CALIB_HBM_COPY)
-            calib = {"mfma_bf16_tflops": round(mf, 1), "hbm_copy_gbps": round(hb, 1),
+            mf16 = rt.calibrate(rt.CALIB_MFMA_BF16_16X16)
+            calib = {"mfma_bf16_tflops": round(mf, 1), "mfma_bf16_16x16x32_tflops": round(mf16, 1),
+                     "hbm_copy_gbps": round(hb, 1),
                      "mfma_frac_of_spec": round(mf / MFMA_BF16_PEAK_TFLOPS, 4),
                      "hbm_frac_of_spec": round(hb / HBM_PEAK_GBPS, 4),
-                     "method": "v_mfma_f32_32x32x16_bf16 chains on random operands, 2 waves/SIMD on every CU; "
+                     "method": "v_mfma_f32_32x32x16_bf16 chains (the fused convs' shape; 16x16x32 beside it) on "
+                               "random operands, 2 waves/SIMD on every CU; "
                                "1 GiB 16-B/lane copy (read + write bytes); best of 3 after a warm launch"}
             if args.precision == "bf16":
                 calib["dominant_frac_of_measured"] = round(roof["achieved"] / mf, 4)

@@ -199,9 +199,10 @@ const char* itsd_kernel_name(int id);
 /* On-box peak calibration (synchronous on stream; measurement only, no reference counterpart):
  * ITSD_CALIB_MFMA_BF16 -> *value = the achievable dense bf16 MFMA rate in TFLOP/s (v_mfma_f32_32x32x16_bf16
  * chains on random operands, every CU, 2 waves per SIMD); ITSD_CALIB_HBM_COPY -> *value = the achievable
- * HBM streaming rate in GB/s (a 1 GiB 16-B-per-lane copy, bytes read + written). bench.py reports its
- * roofline fractions against these as well as against the datasheet peaks. */
-enum { ITSD_CALIB_MFMA_BF16 = 0, ITSD_CALIB_HBM_COPY = 1 };
+ * HBM streaming rate in GB/s (a 1 GiB 16-B-per-lane copy, bytes read + written); ITSD_CALIB_MFMA_BF16_16X16
+ * -> the ITSD_CALIB_MFMA_BF16 loop on v_mfma_f32_16x16x32_bf16 (the chip holds another clock under that shape).
+ * bench.py reports its roofline fractions against these as well as against the datasheet peaks. */
+enum { ITSD_CALIB_MFMA_BF16 = 0, ITSD_CALIB_HBM_COPY = 1, ITSD_CALIB_MFMA_BF16_16X16 = 2 };
 int itsd_calibrate(int what, double* value, void* stream);
 
 const char* itsd_last_error(void);

@@ -1325,7 +1325,7 @@ const char* itsd_last_error(void) { return g_err.c_str(); }
 
 int itsd_calibrate(int what, double* value, void* stream) {
   if (!value) return fail(ITSD_ERR_INVALID, "null argument");
-  if (what != ITSD_CALIB_MFMA_BF16 && what != ITSD_CALIB_HBM_COPY) return fail(ITSD_ERR_INVALID, "unknown calibration");
+  if (what != ITSD_CALIB_MFMA_BF16 && what != ITSD_CALIB_HBM_COPY && what != ITSD_CALIB_MFMA_BF16_16X16) return fail(ITSD_ERR_INVALID, "unknown calibration");
   const int rc = calibrate_run(what, value, (hipStream_t)stream);
   if (rc == ITSD_ERR_OOM) return fail(rc, "calibration buffers (2 x 1 GiB)");
   if (rc != ITSD_OK) return fail(rc, "calibration kernel");

@@ -51,6 +51,42 @@ __global__ __launch_bounds__(256, 2) void calib_mfma_kernel(float* out, int iter
   out[gid] = s;
 }
 
+// the same loop on v_mfma_f32_16x16x32_bf16 (16 independent chains a wave, equal FLOP per chain step x 1/2):
+// the chip holds a different clock under the two shapes (MI355X_MICROARCH.md DVFS item 7)
+__global__ __launch_bounds__(256, 2) void calib_mfma16_kernel(float* out, int iters, uint32_t seed) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  auto hash = [](uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+  };
+  auto rnd8 = [&](uint32_t k) {
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)((hash(seed ^ (gid * 64 + k * 8 + e)) & 0x807F) | 0x3F00);
+    return v;
+  };
+  bf16x8 av[4], bv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) av[i] = rnd8(i);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv[j] = rnd8(4 + j);
+  f32x4 acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[c][r] = 0.0f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c & 3], bv[c >> 2], acc[c], 0, 0, 0);
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += acc[c][r];
+  out[gid] = s;
+}
+
 // HBM streaming copy: 16 B a lane loads and stores, 4 independent loads in flight per lane before their
 // stores (a grid-stride loop of single loads leaves each wave one load deep), nontemporal stores
 // (MI355X_MICROARCH.md: float4 copy measured 6.29 TB/s of the 8 TB/s spec); bytes counted = read + written.
@@ -66,7 +102,7 @@ __global__ __launch_bounds__(256) void calib_copy_kernel(const u32x4* __restrict
   }
 }
 
-// what: ITSD_CALIB_MFMA_BF16 -> TFLOP/s, ITSD_CALIB_HBM_COPY -> GB/s (read + written); synchronous on s.
+// what: ITSD_CALIB_MFMA_BF16 (ITSD_CALIB_MFMA_BF16_16X16) -> TFLOP/s, ITSD_CALIB_HBM_COPY -> GB/s (read + written); synchronous on s.
 // Returns ITSD_OK, ITSD_ERR_OOM (buffers) or ITSD_ERR_HIP.
 int calibrate_run(int what, double* value, hipStream_t s) {
   int dev = 0, cus = 256;
@@ -76,18 +112,21 @@ int calibrate_run(int what, double* value, hipStream_t s) {
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return ITSD_ERR_HIP;
   double best = 0.0;
   int rc = 0;
-  if (what == ITSD_CALIB_MFMA_BF16) {
+  if (what == ITSD_CALIB_MFMA_BF16 || what == ITSD_CALIB_MFMA_BF16_16X16) {
+    const bool m16 = what == ITSD_CALIB_MFMA_BF16_16X16;
     const int blocks = 2 * cus, iters = 1 << 15;  // ~8.6e13 FLOP: tens of ms at ~2 PFLOP/s
     float* out = nullptr;
     if (hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) rc = ITSD_ERR_OOM;
     for (int r = 0; r < 4 && !rc; ++r) {  // the first launch warms the clock; the best of the rest
       hipEventRecord(e0, s);
-      hipLaunchKernelGGL(calib_mfma_kernel, dim3(blocks), dim3(256), 0, s, out, iters, 0x9e3779b9u + r);
+      if (m16) hipLaunchKernelGGL(calib_mfma16_kernel, dim3(blocks), dim3(256), 0, s, out, iters, 0x9e3779b9u + r);
+      else hipLaunchKernelGGL(calib_mfma_kernel, dim3(blocks), dim3(256), 0, s, out, iters, 0x9e3779b9u + r);
       hipEventRecord(e1, s);
       if (hipEventSynchronize(e1) != hipSuccess) { rc = ITSD_ERR_HIP; break; }
       float ms = 0.0f;
       hipEventElapsedTime(&ms, e0, e1);
-      const double flops = (double)blocks * 4 /* waves */ * iters * 8 /* MFMAs */ * 32768.0;
+      // (8 MFMAs of 32x32x16 or 16 of 16x16x32 a wave per iteration: 2^18 FLOP either way)
+      const double flops = (double)blocks * 4 /* waves */ * iters * 8 * 32768.0;
       if (r > 0) best = std::max(best, flops / (ms * 1e-3) / 1e12);  // TFLOP/s
     }
     hipFree(out);

@@ -1436,6 +1436,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 // budget. Here a 512-thread block runs 4 MFMA waves (one per SIMD, 64 couts x 128 pixels each:
 // 8 MFMAs per k-step, half the B reads per MFMA, 128 accumulators in AGPRs) beside the same 4
 // halo waves: 2 waves per SIMD, 256 registers each.
+#ifndef ITSD_P4_M16
+#define ITSD_P4_M16 2
+#endif
 constexpr int P4_RING = 6;  // A k-step slots (prefetch distance 5 k-steps = 40 MFMAs); divides the 36 k-steps
                             // of a chunk, so the slots of the next chunk's prefetched steps line up
 constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 MFMAs ahead)
@@ -1466,7 +1469,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   constexpr int HWs = THs * W;  // pixels of one image segment
   constexpr int TPS = 256 / NSEG, RPP = TPS / 8;
   constexpr int ZROW = GNW_BN;  // COMPACT: the zero row
-  constexpr int HALO = COMPACT ? (((GNW_BN + 1) * ROWB + 1023) & ~1023) : NSEG * ITEMS * RPP * ROWB;
+  // M16: the MFMA waves on v_mfma_f32_16x16x32_bf16 (the LDS residual / output tile forms; the sub-pixel and
+  // register-epilogue forms stay on 32x32x16). ITSD_P4_M16: 0 none, 1 the 32x32 level, 2 every RES form
+  constexpr bool M16 = ITSD_P4_M16 >= 1 && RES && !SUB && (AB & 1) == 0 && (W == 32 || ITSD_P4_M16 >= 2);
+  // (COMPACT + M16: a second zero row 64 rows past the first, so that a lane pointed at the zero row reads zeros at
+  // the +64-row immediate offset of its pixel blocks 4..7 too)
+  constexpr int ZROWS = COMPACT ? (M16 ? 65 : 1) : 0;
+  constexpr int HALO = COMPACT ? (((GNW_BN + ZROWS) * ROWB + 1023) & ~1023) : NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(COMPACT ? ITEMS * RPP == HWs : ITEMS * RPP >= HS, "halo items cover the segment");
   // (sub-pixel forms: 4 slots, dividing every phase's k-step count: 16, or 36 / 24 / 24 / 16 live)
@@ -1569,6 +1578,218 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   };
 
   if (wid < 4) {
+    if constexpr (M16) {
+    // ================================================================ MFMA waves, v_mfma_f32_16x16x32_bf16
+    // The same wave tiles (wave w: couts 64*(w & 1) .. +63, pixels 128*(w >> 1) .. +127) as 4 x 8 16x16
+    // accumulators (f32x4: couts 16 ci + 4 kg .. +3 of pixel 16 pj + m, lane = 16 kg + m), 32 MFMAs per
+    // 32-deep k-step, run as two half-steps of 16 (pixel blocks 0-3, 4-7) so that the B buffers stay 4
+    // fragments. Equal cycles per FLOP to 32x32x16, but the chip holds a higher clock under this shape
+    // (MI355X_MICROARCH.md DVFS item 7; the calibration loops of calib.hip measure both on the box).
+    // A fragments come from the 32x32x16 fragment array unchanged: a 16-cout fragment of k32-step s is
+    // lane 16 (ci & 1) + m + 32 (kg & 1) of 32-cout block 2 wm + (ci >> 1), k16-step 2 s + (kg >> 1).
+    const int wm = wid & 1, wn = wid >> 1, m = lane & 15, kg = lane >> 4;
+    static_assert(COMPACT || (W == 32 && NSEG == 1), "halo rows of the 16-pixel blocks from one base");
+    // pixel block j of this lane: COMPACT the tile pixel hb0 + 16 j (column m % W, row hb0 / W + 16 j / W of its
+    // image); else (32 x 32) halo row hb0 + (j >> 1) * W2 + 16 (j & 1) at tap (0, 0) -- one register
+    const int hb0 = COMPACT ? wn * 128 + m : wn * 4 * W2 + m;
+    const uint32_t ablk = (uint32_t)(NTAP * kpt) * 1024;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wfrag, (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t avo0 = (uint32_t)((kg >> 1) * 1024 + (m + 32 * (kg & 1)) * 16) + 2 * wm * ablk, avo1 = avo0 + ablk;
+    auto abase_of = [&](int k) -> uint32_t { return (uint32_t)(tile_c(k) >> 5) * ablk; };
+    constexpr int KS2 = 2 * NTAP, RING2 = 3;  // k32-steps a chunk; A ring slots (prefetch 2 k32-steps = 64 MFMAs)
+    static_assert(KS2 % RING2 == 0, "ring slots repeat per chunk");
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 ra[RING2][4];
+    // half hf of k32-step s's A fragments (ci = 2 hf, 2 hf + 1): tap s >> 1, k16-steps 2 (s & 1) + (kg >> 1)
+    auto load_a = [&](uint32_t base, int st, u32x4 (&dst)[4], int hf) __attribute__((always_inline)) {
+      const uint32_t off = base + (uint32_t)((st >> 1) * kpt + 2 * (st & 1)) * 1024;
+      const uint32_t vo = hf ? avo1 : avo0;
+      if constexpr ((AB & 8) != 0) {
+        dst[2 * hf] = u32x4{(uint32_t)st, 0u, 0u, 0u};
+        dst[2 * hf + 1] = u32x4{(uint32_t)st, 1u, 0u, 0u};
+      } else {
+        dst[2 * hf] = __builtin_amdgcn_raw_buffer_load_b128(wrs, vo, off, 0);
+        dst[2 * hf + 1] = __builtin_amdgcn_raw_buffer_load_b128(wrs, vo + 256, off, 0);
+      }
+    };
+    {
+      const uint32_t ab0 = abase_of(0);
+#pragma unroll
+      for (int s0 = 0; s0 < RING2 - 1; ++s0) {
+        load_a(ab0, s0, ra[s0], 0);
+        load_a(ab0, s0, ra[s0], 1);
+      }
+    }
+    auto init_acc = [&](int kk) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int seg = NSEG == 1 ? 0 : (wn * 128 + j * 16) / HWs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][j] = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * CONV_BM + wm * 64 + 16 * i + 4 * kg);
+      }
+    };
+    stage_addv(0, tid);
+    block_sync();  // B0: stage 0 staged
+    init_acc(0);
+    int q = 0;
+    for (int k = 0; k < ntiles; ++k) {
+      const uint32_t ab = abase_of(k);
+      const uint32_t abn = k + 1 < ntiles ? abase_of(k + 1) : ab;
+      for (int cc = 0; cc < ncc; ++cc, ++q) {
+        const char* hcur = smem + (q & 1) * HALO;
+        const uint32_t nb = cc + 1 < ncc ? ab + (uint32_t)(cc + 1) * 4 * 1024 : abn;
+        const uint32_t cb = ab + (uint32_t)cc * 4 * 1024;
+        STAMP(c0);
+        // a half-step: 16 MFMAs; its 2 A loads, 4 B reads and address VALU in the first gaps
+        auto half_sched = [&]() __attribute__((always_inline)) {
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+#pragma unroll
+          for (int g = 0; g < 10; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        int tb[4];
+        int zad = 0;  // (W = 16: this lane's zero-row address, for the two pixel blocks a wave-uniform tap row leaves)
+        bf16x8 fb[BD][4];
+        // B unit u = (k32-step u >> 1, pixel blocks 4 (u & 1) .. +3): byte (h * 128 + ((kg ^ sw(h)) << 4)) ^ (s2 << 6),
+        // s2 = the step's half of the tap's 64 channels. Four address registers a tap, rebuilt at its first unit:
+        // a pixel block 16 rows (32x32: block 2t + 1 of block 2t) or 64 rows (COMPACT: block j + 4 of block j) on has
+        // the same swizzle (sw = (h >> 1) & 7), so it is an immediate offset (2048 / 8192 B) of its partner's address.
+        // COMPACT: a tap reading outside its image reads a zero row (x: per lane, all blocks -- the zero rows 256 and
+        // 320; y at 16x16: rows -1 / 16 are wave-uniform, block 0 at ky = 0 of wave row 0, block 7 at ky = 2 of wave
+        // row 1 -- those two reads take the zero-row address; their partners are in range)
+        auto rd = [&](int u, int buf) __attribute__((always_inline)) {
+          const int st = u >> 1, hf = u & 1, tap = st >> 1, s2 = st & 1;
+          const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+          if (s2 == 0 && hf == 0) {
+            int p0 = hb0;
+            asm volatile("" : "+v"(p0));  // (rebuilt per tap, not hoisted out of the chunk loop)
+            const int hoff = (int)(hcur - smem);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              int h;
+              if constexpr (COMPACT) {
+                // block t: x = column, y = row in its image (y range checked at 8x8 only: 16x16 rows are wave-uniform)
+                const int x = (p0 & (W - 1)) + kx - 1, y = (((p0 / W) + t * (16 / W)) & (W - 1)) + ky - 1;
+                const bool ok = (unsigned)x < (unsigned)W && (W == 16 || (unsigned)y < (unsigned)W);
+                h = ok ? p0 + 16 * t + (ky - 1) * W + (kx - 1) : ZROW;
+              } else {
+                h = p0 + t * W2 + ky * W2 + kx;  // block 2t
+              }
+              tb[t] = hoff + h * ROWB + ((kg ^ ((h >> 1) & 7)) << 4);
+            }
+            if constexpr (COMPACT && W == 16)
+              if (ky != 1) zad = hoff + ZROW * ROWB + ((kg ^ ((ZROW >> 1) & 7)) << 4);
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * hf + jj;
+            int ad;
+            if constexpr (COMPACT) {
+              ad = (tb[jj] ^ (s2 << 6)) + hf * 8192;
+              if constexpr (W == 16) {
+                if (ky == 0 && j == 0 && wn == 0) ad = zad ^ (s2 << 6);
+                if (ky == 2 && j == 7 && wn == 1) ad = zad ^ (s2 << 6);
+              }
+            } else {
+              ad = (tb[j >> 1] ^ (s2 << 6)) + (j & 1) * 2048;
+            }
+            if constexpr ((AB & 16) != 0) fb[buf][jj] = bf16x8{(short)(u + jj), 0, 0, 0, 0, 0, 0, 1};
+            else fb[buf][jj] = *(const bf16x8*)(smem + ad);
+          }
+        };
+#pragma unroll
+        for (int u0 = 0; u0 < BD - 1; ++u0) rd(u0, u0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 2 * KS2; ++u) {
+          const int st = u >> 1, hf = u & 1, pf = st + RING2 - 1;
+          if (pf < KS2) load_a(cb, pf, ra[pf % RING2], hf);
+          else load_a(nb, pf - KS2, ra[pf % RING2], hf);
+          if (u + BD - 1 < 2 * KS2) rd(u + BD - 1, (u + BD - 1) % BD);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 af = __builtin_bit_cast(bf16x8, ra[st % RING2][i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fb[u % BD][j], acc[i][4 * hf + j], 0, 0, 0);
+          }
+          half_sched();
+        }
+        STAMP(c1);
+        STAMP_ADD(0, c1 - c0);
+        block_sync();  // end of stage q: its buffer is free, stage q+1 is published
+      }
+      STAMP(e0);
+      if constexpr ((AB & 4) == 0) {
+        // epilogue of tile k into the LDS residual / output tile (the 32x32x16 path's layout: row p, 16-B group
+        // cout / 8 ^ sw(p), 8-B half (cout / 4) & 1); the halo waves store it and sum its statistics
+        auto epi = [&](auto hr) __attribute__((always_inline)) {
+          constexpr bool HR = decltype(hr)::value;
+          uint2 rr[2][4];
+          int pb = wn * 128 + m, kgo = kg;
+          asm volatile("" : "+v"(pb), "+v"(kgo));  // (the 32 addresses are rebuilt here, not held through the chunk loop)
+          auto addr = [&](int i, int j) {
+            const int p = pb + j * 16;
+            return rlds + wm * 32768 + p * 128 + (((2 * i + (kgo >> 1)) ^ ((p >> 1) & 7)) << 4) + 8 * (kgo & 1);
+          };
+          auto rdr = [&](int j, uint2 (&d)[4]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d[i] = HR ? *(const uint2*)addr(i, j) : uint2{0u, 0u};
+          };
+          rdr(0, rr[0]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (j + 1 < 8) rdr(j + 1, rr[(j + 1) & 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint2 r = rr[j & 1][i];
+              const float v0 = acc[i][j][0] + __uint_as_float(r.x << 16);
+              const float v1 = acc[i][j][1] + __uint_as_float(r.x & 0xffff0000u);
+              const float v2 = acc[i][j][2] + __uint_as_float(r.y << 16);
+              const float v3 = acc[i][j][3] + __uint_as_float(r.y & 0xffff0000u);
+              *(uint2*)addr(i, j) = uint2{pk_bf16(v0, v1), pk_bf16(v2, v3)};
+            }
+          }
+        };
+        if (a.resid) epi(std::true_type{});
+        else epi(std::false_type{});
+      } else {  // keep the accumulators alive
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm += acc[i][j][r];
+        if (sm == 1.2345f) ((float*)a.out)[0] = sm;
+      }
+      if (k + 1 < ntiles) init_acc(k + 1);
+      STAMP(e1);
+      STAMP_ADD(6, e1 - e0);
+    }
+    block_sync();  // the last tile's output is in LDS
+    P4_STAMP_OUT();
+    return;
+    } else {
     // ================================================================ MFMA waves (one per SIMD)
     // wave w: couts 64*(w & 1) .. +63 (two 32-cout A fragments per k-step), pixels 128*(w >> 1) ..
     // +127 (four B fragments): 8 MFMAs per k-step on 128 accumulator registers (AGPRs)
@@ -1924,6 +2145,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     if constexpr (RES) block_sync();  // the last tile's output is in LDS
     P4_STAMP_OUT();
     return;
+    }  // (!M16)
   }
 
   // ================================================================== halo waves
@@ -2242,6 +2464,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   }
   if constexpr (COMPACT) {  // the zero row of both halo buffers (no stage writes it; read after B0)
     if (tt < 16) *(u32x4*)(smem + (tt >> 3) * HALO + ZROW * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
+    if (M16 && tt >= 16 && tt < 32)
+      *(u32x4*)(smem + ((tt >> 3) & 1) * HALO + (ZROW + 64) * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
   }
   emit(smem);
 #ifdef ITSD_STAMPS

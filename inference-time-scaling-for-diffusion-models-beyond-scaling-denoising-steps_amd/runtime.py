@@ -248,11 +248,12 @@ def noise(out: torch.Tensor, n_cand: int, seed: int, stream_id: int, cand_offset
     return out
 
 
-CALIB_MFMA_BF16, CALIB_HBM_COPY = 0, 1
+CALIB_MFMA_BF16, CALIB_HBM_COPY, CALIB_MFMA_BF16_16X16 = 0, 1, 2
 
 
 def calibrate(what: int) -> float:
-    """On-box achievable peak: CALIB_MFMA_BF16 -> TFLOP/s, CALIB_HBM_COPY -> GB/s (itsd_calibrate)."""
+    """On-box achievable peak: CALIB_MFMA_BF16 (32x32x16) / CALIB_MFMA_BF16_16X16 -> TFLOP/s, CALIB_HBM_COPY -> GB/s
+    (itsd_calibrate)."""
     v = ctypes.c_double(0.0)
     check(lib().itsd_calibrate(int(what), ctypes.byref(v), stream_ptr()))
     return v.value

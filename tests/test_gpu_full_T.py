@@ -22,8 +22,11 @@ DESIGN.md section 4). Two drifts of the oracle's own whole loop on CPU:
   bf16   a bf16 emulation of the oracle (weights bf16; every conv's input and output rounded to bf16 with
          fp32 accumulation, as the GPU's bf16 path) against the fp32 oracle: the GPU bf16 path and the
          emulation are two bf16 evaluations of one fp32 trajectory; bound = 2 x the emulation's drift.
-         C2 T=1000: x0 rel-L2 3.0e-2 -> 6.1e-2, score 1.1e-4 -> 2.2e-4; C5 T=3000: see the JSON (the T=3000
-         images of the synthetic model saturate to +-1, so their rel-L2 counts sign flips: 2 sqrt(k / 3072)).
+         C2 T=1000: x0 rel-L2 3.0e-2 -> 6.1e-2; C5 T=3000: see the JSON (the T=3000 images of the synthetic
+         model saturate to +-1, so their rel-L2 counts sign flips: 2 sqrt(k / 3072)).
+  scores an exact consequence of the image (_check_score): the search's score equals the verifier on the
+         candidate's own x0 (1e-6), and differs from the oracle trajectory's score by at most what the measured
+         x0 difference implies (Cauchy-Schwarz on the variance; no sampled bound).
 Measured values are printed.
 """
 import dataclasses
@@ -63,6 +66,28 @@ ENGINE_SEED = 21
 
 def _rel_l2(a, b):
     return (torch.linalg.norm((a - b).flatten()) / torch.linalg.norm(b.flatten())).item()
+
+
+def _check_score(tag, got_x0, got_score, ref_x0, sampled_bound):
+    """The OracleVerifier score of a candidate, in two exact steps (no sampled bound):
+    (1) the search's score IS the verifier on the candidate's own image: |score - R.oracle_score(x0)| <= 1e-6;
+    (2) against the oracle trajectory's score, the difference the image difference implies: with d = x0 - ref,
+        var(ref + d) - var(ref) = 2 cov(ref, d) + var(d) and |cov| <= std(ref) std(d) (Cauchy-Schwarz), and
+        1/(1+v1) - 1/(1+v2) = (v2 - v1) / ((1+v1)(1+v2)), so |ds| <= (2 std(ref) std(d) + var(d)) / ((1+v1)(1+v2)).
+    The image itself is bounded by the derived rel-L2 tolerance beside this call. (Round 5: the sampled bound
+    -- 2 x the largest score drift of 3 bf16-emulation images -- was exceeded at T = 3000, 7.5e-5 vs 6.3e-5, by
+    a candidate whose x0 was inside its derived bound: 3 samples do not bound a tail; it is printed, not asserted.)"""
+    g, r = got_x0.flatten().double(), ref_x0.flatten().double()
+    d = g - r
+    self_score = R.oracle_score(got_x0.unsqueeze(0).float())
+    assert abs(float(got_score) - self_score) <= 1e-6, (tag, float(got_score), self_score)
+    v1, v2 = torch.var(r).item(), torch.var(g).item()
+    implied = (2 * torch.std(r).item() * torch.std(d).item() + torch.var(d).item()) / ((1 + v1) * (1 + v2))
+    s_ref = R.oracle_score(ref_x0.unsqueeze(0))
+    ds = abs(float(got_score) - s_ref)
+    print(f"{tag}: score {float(got_score):.6f} (verifier on its own x0 {self_score:.6f}) vs oracle {s_ref:.6f}: "
+          f"|d| {ds:.2e}, implied by the x0 difference <= {implied:.2e} (sampled emulation figure {sampled_bound:.2e})")
+    assert ds <= implied * (1 + 1e-6) + 1e-7
 
 
 @pytest.fixture(scope="module")
@@ -136,12 +161,9 @@ def test_C2_bf16_round_T1000_candidates_and_scores_vs_oracle(full_T):
         ref = full_T["oracle_x0"][3 + k]
         got = c2["x0"][i]
         rel = _rel_l2(got, ref)
-        s_ref = R.oracle_score(ref.unsqueeze(0))
-        ds = abs(float(c2["scores"][i]) - s_ref)
-        print(f"C2 bf16 candidate {i}: x0 rel-L2 {rel:.3e}, max|d| {(got - ref).abs().max().item():.3e}; "
-              f"score {float(c2['scores'][i]):.6f} vs oracle {s_ref:.6f} (|d| {ds:.2e})")
+        print(f"C2 bf16 candidate {i}: x0 rel-L2 {rel:.3e}, max|d| {(got - ref).abs().max().item():.3e}")
         assert rel <= FULL_T_BF16_REL_L2
-        assert ds <= FULL_T_BF16_SCORE
+        _check_score(f"C2 candidate {i}", got, c2["scores"][i], ref, FULL_T_BF16_SCORE)
 
 
 C5_T, C5_N, C5_CANDS, C5_SEED = 3000, 128, (0, 64, 127), 33
@@ -180,12 +202,9 @@ def test_C5_path_search_round_T3000_candidates_and_scores_vs_oracle():
         ref = R.p_sample_loop(fw, x_T, R.schedule(1e-4, 0.02, C5_T), noise)
     for k, i in enumerate(C5_CANDS):
         rel = _rel_l2(x0[i], ref[k])
-        s_ref = R.oracle_score(ref[k:k + 1])
-        ds = abs(float(scores[i]) - s_ref)
-        print(f"C5 bf16 path candidate {i}: T=3000 x0 rel-L2 {rel:.3e}, max|d| {(x0[i] - ref[k]).abs().max().item():.3e}; "
-              f"score {float(scores[i]):.6f} vs oracle {s_ref:.6f} (|d| {ds:.2e})")
+        print(f"C5 bf16 path candidate {i}: T=3000 x0 rel-L2 {rel:.3e}, max|d| {(x0[i] - ref[k]).abs().max().item():.3e}")
         assert rel <= C5_BF16_REL_L2
-        assert ds <= C5_BF16_SCORE
+        _check_score(f"C5 candidate {i}", x0[i], scores[i], ref[k], C5_BF16_SCORE)
 
 
 def test_C1c_main_condition_eval_T1000_fp32_vs_oracle(tmp_path):
