@@ -1246,6 +1246,11 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p4_xcd = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "p4_c96")) {  // 8x8 conv3x3_gn_p4_kernel on 96-cout tiles: 0 off, 1 auto, 2 always (Cout % 96 == 0)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p4_c96 in [0,2]");
+    itsd::g_p4_c96 = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p4_sub")) {  // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form: 0 off, 1 on
     if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_sub in [0,1]");
     itsd::g_p4_sub = value;

@@ -26,6 +26,7 @@ extern int g_small_minks;  // conv_small split K: >= this many K-chunks a slice 
 extern int g_convt_prune;  // ConvTranspose2d sub-pixel phases skip their all-zero taps: 0 off, 1 on ("convt_prune")
 extern int g_subpix_split;  // under-filled sub-pixel conv_pipe launches split K in-launch: 0 off, 1 on ("subpix_split")
 extern int g_p4_xcd;        // persistent fused convs: contiguous tile ranges per XCD ("p4_xcd")
+extern int g_p4_c96;        // 8x8 conv3x3_gn_p4_kernel<8, 512> (96-cout tiles): 0 off, 1 auto, 2 always (itsd_set_option "p4_c96")
 extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")

@@ -58,6 +58,7 @@ int g_small_minks = 8;    // conv_small split K: >= this many K-chunks a slice (
 int g_convt_prune = 1;    // ConvTranspose2d sub-pixel phases skip their all-zero taps (itsd_set_option "convt_prune")
 int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
 int g_p4_xcd = 0;        // conv3x3_gn_p4_kernel: each XCD a contiguous range of tiles (ConvArgs::xcd)
+int g_p4_c96 = 1;        // 8x8 p4 on 96-cout tiles where they fill the CUs better: 0 off, 1 auto, 2 always (conv_p4_c96)
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
@@ -1475,6 +1476,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // (COMPACT + M16: a second zero row 64 rows past the first, so that a lane pointed at the zero row reads zeros at
   // the +64-row immediate offset of its pixel blocks 4..7 too)
   constexpr int ZROWS = COMPACT ? (M16 ? 65 : 1) : 0;
+  // C96 (AB bit 512, 8x8 only): 96-cout tiles -- Cout = 384 gives 4 cout tiles, so N = 256's 64 pixel tiles make
+  // 256 tiles for the 256 CUs instead of 192 with 128 couts (a quarter of the chip idle). Each MFMA wave holds 48
+  // couts (3 16x16 blocks); the LDS output tile keeps its 64-cout halves (48 used: units 0..5 of 8)
+  constexpr bool C96 = (AB & 512) != 0;
+  constexpr int BM = C96 ? 96 : CONV_BM, HB = BM / 2, NCI = HB / 16;
+  static_assert(!C96 || (M16 && COMPACT), "96-cout tiles: the 16x16x32 compact forms");
   constexpr int HALO = COMPACT ? (((GNW_BN + ZROWS) * ROWB + 1023) & ~1023) : NSEG * ITEMS * RPP * ROWB;
   constexpr int RESB = RES ? GNW_BN * CONV_BM * 2 : 0;  // residual tile, bf16 [256 px][128 couts]
   static_assert(COMPACT ? ITEMS * RPP == HWs : ITEMS * RPP >= HS, "halo items cover the segment");
@@ -1497,7 +1504,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.Hout;
   const int Cin = a.C1 + a.C2, ncc = Cin / 64, kpt = Cin >> 4;
-  const int nTC = a.Cout / CONV_BM, nPT = a.M / GNW_BN, NT = (SUB ? 4 : 1) * nPT * nTC;
+  const int nTC = a.Cout / BM, nPT = a.M / GNW_BN, NT = (SUB ? 4 : 1) * nPT * nTC;
   // xcd: blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one; speed only), so logical
   // block (b % 8) * G/8 + b / 8 gives each XCD a contiguous eighth of the tile sequence: the cout tiles of a
   // pixel tile (8x8: 3 blocks) read its input through one L2 instead of three
@@ -1521,7 +1528,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     return t % Q;
   };
   auto tile_p = [&](int k) { return (tile_r(k) / nTC) * GNW_BN; };
-  auto tile_c = [&](int k) { return (tile_r(k) % nTC) * CONV_BM; };
+  auto tile_c = [&](int k) { return (tile_r(k) % nTC) * BM; };
   auto tile_ph = [&](int k) -> int {
     const int t = tb0 + k;
     if constexpr (!SUB) return 0;
@@ -1564,8 +1571,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   auto stage_addv = [&](int k, int t0) {  // threads t0 .. t0+255
     const int tileP = tile_p(k), tileC = tile_c(k), img0 = tileP / (H * W);
     const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = t0; it < NSEG * CONV_BM; it += 256) {
-      const int il = it / CONV_BM, cl = it % CONV_BM, co = tileC + cl, img = img0 + il;
+    for (int it = t0; it < NSEG * BM; it += 256) {
+      const int il = it / BM, cl = it - il * BM, co = tileC + cl, img = img0 + il;
       float v = a.bias[co];
       if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
       if (a.cemb) {
@@ -1573,7 +1580,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         if (a.cemb_uncond_from < 0 || img < a.cemb_uncond_from) lab = a.cemb_labels[img % a.cemb_label_mod];
         v += a.cemb[(long long)lab * a.cemb_row_stride + co];
       }
-      addv[(k & 1) * NSEG * CONV_BM + it] = v;
+      addv[(k & 1) * NSEG * BM + it] = v;
     }
   };
 
@@ -1598,20 +1605,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     auto abase_of = [&](int k) -> uint32_t { return (uint32_t)(tile_c(k) >> 5) * ablk; };
     constexpr int KS2 = 2 * NTAP, RING2 = 3;  // k32-steps a chunk; A ring slots (prefetch 2 k32-steps = 64 MFMAs)
     static_assert(KS2 % RING2 == 0, "ring slots repeat per chunk");
-    f32x4 acc[4][8];
+    f32x4 acc[NCI][8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NCI; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    u32x4 ra[RING2][4];
+    u32x4 ra[RING2][NCI];
+    // C96: the wave's 16-cout block b is block 3 wm + b of the tile -- 32-cout block (3 wm + b) >> 1, half
+    // (3 wm + b) & 1: a wave-uniform part of the offset, added to soffset
+    const uint32_t avl = (uint32_t)((kg >> 1) * 1024 + (m + 32 * (kg & 1)) * 16);
+    auto fo96 = [&](int b) -> uint32_t { return (uint32_t)((3 * wm + b) >> 1) * ablk + (uint32_t)((3 * wm + b) & 1) * 256; };
     // half hf of k32-step s's A fragments (ci = 2 hf, 2 hf + 1): tap s >> 1, k16-steps 2 (s & 1) + (kg >> 1)
-    auto load_a = [&](uint32_t base, int st, u32x4 (&dst)[4], int hf) __attribute__((always_inline)) {
+    auto load_a = [&](uint32_t base, int st, u32x4 (&dst)[NCI], int hf) __attribute__((always_inline)) {
       const uint32_t off = base + (uint32_t)((st >> 1) * kpt + 2 * (st & 1)) * 1024;
-      const uint32_t vo = hf ? avo1 : avo0;
       if constexpr ((AB & 8) != 0) {
-        dst[2 * hf] = u32x4{(uint32_t)st, 0u, 0u, 0u};
-        dst[2 * hf + 1] = u32x4{(uint32_t)st, 1u, 0u, 0u};
+#pragma unroll
+        for (int b = 2 * hf; b < 2 * hf + 2; ++b)
+          if (b < NCI) dst[b] = u32x4{(uint32_t)st, (uint32_t)b, 0u, 0u};
+      } else if constexpr (C96) {
+#pragma unroll
+        for (int b = 2 * hf; b < 2 * hf + 2; ++b)
+          if (b < NCI) dst[b] = __builtin_amdgcn_raw_buffer_load_b128(wrs, avl, off + fo96(b), 0);
       } else {
+        const uint32_t vo = hf ? avo1 : avo0;
         dst[2 * hf] = __builtin_amdgcn_raw_buffer_load_b128(wrs, vo, off, 0);
         dst[2 * hf + 1] = __builtin_amdgcn_raw_buffer_load_b128(wrs, vo + 256, off, 0);
       }
@@ -1629,8 +1645,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       for (int j = 0; j < 8; ++j) {
         const int seg = NSEG == 1 ? 0 : (wn * 128 + j * 16) / HWs;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[i][j] = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * CONV_BM + wm * 64 + 16 * i + 4 * kg);
+        for (int i = 0; i < NCI; ++i)
+          acc[i][j] = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * BM + wm * HB + 16 * i + 4 * kg);
       }
     };
     stage_addv(0, tid);
@@ -1726,7 +1742,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
           else load_a(nb, pf - KS2, ra[pf % RING2], hf);
           if (u + BD - 1 < 2 * KS2) rd(u + BD - 1, (u + BD - 1) % BD);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < NCI; ++i) {
             const bf16x8 af = __builtin_bit_cast(bf16x8, ra[st % RING2][i]);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -1744,23 +1760,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         // cout / 8 ^ sw(p), 8-B half (cout / 4) & 1); the halo waves store it and sum its statistics
         auto epi = [&](auto hr) __attribute__((always_inline)) {
           constexpr bool HR = decltype(hr)::value;
-          uint2 rr[2][4];
+          uint2 rr[2][NCI];
           int pb = wn * 128 + m, kgo = kg;
           asm volatile("" : "+v"(pb), "+v"(kgo));  // (the 32 addresses are rebuilt here, not held through the chunk loop)
           auto addr = [&](int i, int j) {
             const int p = pb + j * 16;
             return rlds + wm * 32768 + p * 128 + (((2 * i + (kgo >> 1)) ^ ((p >> 1) & 7)) << 4) + 8 * (kgo & 1);
           };
-          auto rdr = [&](int j, uint2 (&d)[4]) __attribute__((always_inline)) {
+          auto rdr = [&](int j, uint2 (&d)[NCI]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) d[i] = HR ? *(const uint2*)addr(i, j) : uint2{0u, 0u};
+            for (int i = 0; i < NCI; ++i) d[i] = HR ? *(const uint2*)addr(i, j) : uint2{0u, 0u};
           };
           rdr(0, rr[0]);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if (j + 1 < 8) rdr(j + 1, rr[(j + 1) & 1]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < NCI; ++i) {
               const uint2 r = rr[j & 1][i];
               const float v0 = acc[i][j][0] + __uint_as_float(r.x << 16);
               const float v1 = acc[i][j][1] + __uint_as_float(r.x & 0xffff0000u);
@@ -1775,7 +1791,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
       } else {  // keep the accumulators alive
         float sm = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NCI; ++i)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -1855,7 +1871,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
           for (int j = 0; j < 4; ++j) {
             // (the image segment of pixel block j: NSEG = 4 -- 64-pixel images -- has two a wave)
             const int seg = NSEG == 1 ? 0 : (wn * 128 + j * 32) / HWs;
-            const f32x4 ad = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * CONV_BM + (2 * wm + i) * 32 + 8 * g + 4 * hh);
+            const f32x4 ad = *(const f32x4*)(addv + ((kk & 1) * NSEG + seg) * BM + (2 * wm + i) * 32 + 8 * g + 4 * hh);
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = ad[e];
           }
@@ -2032,14 +2048,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
       const int wmi = 2 * wm + i;
-      const float* av = addv + (k & 1) * NSEG * CONV_BM + wmi * 32 + 4 * hh;
+      const float* av = addv + (k & 1) * NSEG * BM + wmi * 32 + 4 * hh;
       float s16[16], q16[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int p = wn * 128 + j * 32 + rl;
-        const float* avj = av + (NSEG == 1 ? 0 : (wn * 2 + (j >> 1))) * CONV_BM;
+        const float* avj = av + (NSEG == 1 ? 0 : (wn * 2 + (j >> 1))) * BM;
         uint32_t wv[4][2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -2294,7 +2310,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {  // rows 128 ds + 8 i + lane / 8; LDS unit lane % 8 <- source unit u
         const int row = 128 * ds + 8 * i + (lane >> 3), u = (lane & 7) ^ ((row >> 1) & 7);
-        const T* src = (const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + dh * 64 + u * 8;
+        // (C96: units 6, 7 of a half are past its 48 couts -- those lanes load unit 0 again, never read)
+        const int us = (C96 && u >= HB / 8) ? 0 : u;
+        const T* src = (const T*)a.resid + (size_t)(tileP + row) * a.Cout + tileC + dh * HB + us * 8;
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(rlds + dh * 32768 + (128 * ds + 8 * i) * 128), 16, 0, 0);
       }
     }
@@ -2320,8 +2338,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = hf * 16 / NH; i < (hf + 1) * 16 / NH; ++i) {
           const int row = 128 * ds + 8 * i + (lane >> 3);
-          const u32x4 d = *(const u32x4*)(rlds + dh * 32768 + row * 128 + ((u ^ ((row >> 1) & 7)) << 4));
-          *(u32x4*)((T*)a.out + orow(tileP + row, dph) * a.Cout + tileC + dh * 64 + u * 8) = d;
+          u32x4 d = *(const u32x4*)(rlds + dh * 32768 + row * 128 + ((u ^ ((row >> 1) & 7)) << 4));
+          if (!C96 || u < HB / 8) *(u32x4*)((T*)a.out + orow(tileP + row, dph) * a.Cout + tileC + dh * HB + u * 8) = d;
+          else d = u32x4{0u, 0u, 0u, 0u};  // (C96: no such couts; zeros through the statistics butterfly)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             const float lo = __uint_as_float(d[w] << 16), hi = __uint_as_float(d[w] & 0xffff0000u);
@@ -2359,8 +2378,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
             const int HWi = H * W, spp = HWi / 128, img = tileP / HWi;
             slot = (long long)img * 4 * spp + dph * spp + (tileP - img * HWi) / 128 + ds;
           }
-          const int co = dh * 64 + 8 * u + 4 * ((lane >> 4) & 1) + 2 * (lane >> 5);
-          *(float2*)(a.stats + (slot * 2 + ((lane >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
+          const int co = dh * HB + 8 * u + 4 * ((lane >> 4) & 1) + 2 * (lane >> 5);
+          if (!C96 || u < HB / 8) *(float2*)(a.stats + (slot * 2 + ((lane >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
         }
       }
     }
@@ -2550,6 +2569,9 @@ template <int W> struct Gp5Cfg {
 constexpr int P5_RING = 9;  // A k-step slots (prefetch distance 8 k-steps = 32 MFMAs); divides 36
                             // (12 and 18 measured equal at N = 32 and 256)
 constexpr int P5_BD = 3;    // B fragment buffers (reads two k-steps = 8 MFMAs ahead)
+// (round 5: the MFMA waves on v_mfma_f32_16x16x32_bf16 as in p4 -- 2 x 8 f32x4 accumulators, 6-slot k32 A ring, 8-B
+// stores, per-slot butterflies over the 16 pixel lanes -- measured N = 256 equal, N = 32 +2.3 %, N = 64 +0.7 %, C4
+// +0.7 % step time against this form, profiles/r05/step_p5_m16_vs_m32.txt: removed)
 
 template <int W>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
@@ -3376,8 +3398,19 @@ static int p5_split(const ConvArgs& a, int tiles, int nch) {
 
 bool conv_p5_selected(const ConvArgs& a);
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p4_kernel (any form)?
+// 96-cout tiles of conv3x3_gn_p4_kernel<8> (AB 512)? Where the 128-cout tile count leaves CUs idle and 96-cout
+// tiles need fewer tile-rounds x tile cost (ceil(NT / CUs) x BM / 128), e.g. N = 256: 192 -> 256 tiles
+bool conv_p4_c96(const ConvArgs& a) {
+  if (!g_p4_c96 || a.Wout != 8 || a.Cout % 96 || a.M % GNW_BN || ITSD_P4_M16 < 2) return false;
+  const long long npt = a.M / GNW_BN, G = g_num_cus;
+  const long long t96 = npt * (a.Cout / 96), r96 = (t96 + G - 1) / G;
+  if (a.Cout % CONV_BM) return true;
+  const long long t128 = npt * (a.Cout / CONV_BM), r128 = (t128 + G - 1) / G;
+  return g_p4_c96 == 2 || 3 * r96 * 100 < 4 * r128 * 97;  // 0.75 r96 < 0.97 r128
+}
 bool conv_p4_selected(const ConvArgs& a) {
   if (!a.gn_coef || conv_p5_selected(a) || !conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) return false;
+  if (conv_p4_c96(a)) return a.wfrag && a.Hout == a.Wout && a.C1 + a.C2 >= 128 && (g_p4_w & 1);
   return a.wfrag && a.Cout % CONV_BM == 0 && a.Hout == a.Wout && a.C1 + a.C2 >= 128 &&
          ((a.Wout == 32 && (g_p4_w & 4)) || (a.Wout == 16 && (g_p4_w & 2)) || (a.Wout == 8 && (g_p4_w & 1)));
 }
@@ -3461,13 +3494,15 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
       if (const int segs = conv_gn_wide_segs(a.Hout, a.Wout, a.M, a.Cout)) {
         if (conv_p4_selected(a)) {
           // persistent, one MFMA wave per SIMD (512 threads, 256 registers a wave)
-          const int tiles = (a.M / GNW_BN) * (a.Cout / CONV_BM);
+          const bool c96 = conv_p4_c96(a);
+          const int tiles = (a.M / GNW_BN) * (a.Cout / (c96 ? 96 : CONV_BM));
           const dim3 gp(std::min(tiles, g_num_cus));
 #ifdef ITSD_DIAG
           if ((g_conv_dbg & 4096) && a.Wout == 32) return launch_p4_ablation(a, gp, s);
 #endif
           if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p4_kernel<32>, gp, dim3(512), 0, s, a);
           else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p4_kernel<16>, gp, dim3(512), 0, s, a);
+          else if (c96) ITSD_LAUNCH((conv3x3_gn_p4_kernel<8, 512>), gp, dim3(512), 0, s, a);
           else ITSD_LAUNCH(conv3x3_gn_p4_kernel<8>, gp, dim3(512), 0, s, a);
           return hipGetLastError();
         }

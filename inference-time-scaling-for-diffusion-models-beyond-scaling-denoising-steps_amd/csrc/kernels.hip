@@ -378,6 +378,18 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
     const int u = tid + 512 * i, t = u / (C / 8), ch = u - t * (C / 8);
     xv[i] = *(const u32x4*)(x + (size_t)t * C + ch * 8);
   }
+  // (round 5) every weight stream's first PF fragments are issued ahead of its phase: phase 1's here, behind the
+  // x loads (they arrive during the group statistics and hn staging), phase 2's chunk 0 in phase 1's last PF
+  // steps and chunk c + 1 after chunk c's Q / K stores, phase 5's before the softmax -- no phase opens with a
+  // memory round trip
+  constexpr int NBW = (CB + 7) / 8;
+  bf16x8 bw[PF][NBW];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+      if (w + 8 * b < CB) bw[p][b] = *frag(a.wqkv, 2 * CB + w + 8 * b, p);
+  bf16x8 fa[PF];  // phase 2's ring (Q / K weights of channel block 4 ch + w % 4)
   float* gs = (float*)(sm + R_GS);  // [32 groups][mean, rstd]
   if (tid < 256) {
     const int g = tid >> 3, l8 = tid & 7, gsz = C / 32, n_it = gsz * a.spi;
@@ -432,7 +444,6 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
   // channel group used to stream the same fragments): V^T and proj -- channel blocks w, w + 8 (NBW a
   // wave at most); q|k -- wave w computes Q (w < 4) or K (w >= 4) of block 4 ch + w % 4. Every
   // output's k order is unchanged.
-  constexpr int NBW = (CB + 7) / 8;
   // ---- 1. V^T: D[token][c] = hn Wv^T; wave w: channel blocks w + 8 b x both token blocks
   {
     f32x16 acc[2][NBW];
@@ -442,21 +453,18 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       for (int b = 0; b < NBW; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[tb][b][r] = 0.f;
-    bf16x8 bw[PF][NBW];
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-#pragma unroll
-      for (int b = 0; b < NBW; ++b)
-        if (w + 8 * b < CB) bw[p][b] = *frag(a.wqkv, 2 * CB + w + 8 * b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       bf16x8 cur[NBW];
 #pragma unroll
       for (int b = 0; b < NBW; ++b) cur[b] = bw[st % PF][b];
-      if (st + PF < KS)
+      if (st + PF < KS) {
 #pragma unroll
         for (int b = 0; b < NBW; ++b)
           if (w + 8 * b < CB) bw[st % PF][b] = *frag(a.wqkv, 2 * CB + w + 8 * b, st + PF);
+      } else {
+        fa[st + PF - KS] = *frag(a.wqkv, (w >> 2) * CB + wq, st + PF - KS);
+      }
 #pragma unroll
       for (int tb = 0; tb < 2; ++tb) {
         const bf16x8 h0 = hn_frag(32 * tb + rl, st);
@@ -494,9 +502,6 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) aa[tb][r] = 0.f;
-      bf16x8 fa[PF];
-#pragma unroll
-      for (int p = 0; p < PF; ++p) fa[p] = *frag(a.wqkv, cb, p);
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
         const bf16x8 w_ = fa[st % PF];
@@ -518,6 +523,10 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
           *(uint2*)(dstc + rowc(tk, 4 * wq + g, 256) + 8 * hh) =
               uint2{pk_bf16(aa[tb][4 * g] + bq[0], aa[tb][4 * g + 1] + bq[1]), pk_bf16(aa[tb][4 * g + 2] + bq[2], aa[tb][4 * g + 3] + bq[3])};
         }
+      // the next chunk's first PF fragments, in flight through this chunk's barriers and score MFMAs
+      if (ch + 1 < NCH)
+#pragma unroll
+        for (int p = 0; p < PF; ++p) fa[p] = *frag(a.wqkv, cb + 4, p);
     }
     __syncthreads();
     if (w < 4) {
@@ -532,6 +541,13 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
     __syncthreads();  // Q_c / K_c are rewritten by the next chunk
   }
   ATL(3);  // scores done
+  // phase 5's first PF weight fragments, in flight through the softmax and PV phases
+  bf16x8 aw[PF][NBW];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+      if (w + 8 * b < CB) aw[p][b] = *frag(a.wp, w + 8 * b, p);
   // ---- 3. softmax over keys: S[query][key] fp32 through LDS, P [query][key] bf16
   float* const Sm = (float*)(sm + R_QK);              // [64][64 + 4]
   char* const Pm = sm + R_QK + S * (S + 4) * 4;       // [64][64] bf16, 128-B rows
@@ -605,12 +621,6 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
       for (int b = 0; b < NBW; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[tb][b][r] = 0.f;
-    bf16x8 aw[PF][NBW];
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-#pragma unroll
-      for (int b = 0; b < NBW; ++b)
-        if (w + 8 * b < CB) aw[p][b] = *frag(a.wp, w + 8 * b, p);
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
       bf16x8 cur[NBW];

@@ -633,6 +633,35 @@ def test_streaming_1x1_convs_vs_conv_pipe_n256():
     assert _rel_l2(st[idx], ref) < REL_L2_BF16
 
 
+def test_p4_96_cout_tiles_bit_identical_n256():
+    """The 8x8 fused convs of the bench batch on 96-cout tiles (conv3x3_gn_p4_kernel<8, 512>: 256 tiles for the
+    256 CUs instead of 192): every output's MFMA k order and every statistics slot's row order are the
+    128-cout tiles', so the forward is bit-identical to p4_c96 = 0; and vs the oracle on images at both ends."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    n = 256
+    gen = torch.Generator().manual_seed(960)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    assert any("<8, 512>" in o["kernel"] for o in ops), sorted({o["kernel"] for o in ops})
+
+    def run(v):
+        rt.set_option("p4_c96", v)
+        try:
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("p4_c96", 1)
+
+    c96 = run(1)
+    assert torch.equal(c96, run(1))
+    assert torch.equal(c96, run(0))
+    idx = [0, 255]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    assert _rel_l2(c96[idx], ref) < REL_L2_BF16
+
+
 def test_forward_bf16_full_batch_vs_oracle_subset():
     """The bench batch (N=256) runs the persistent fused convs with several tiles per block
     (4 at 32x32, 2 at 16x16), the 2-blocks-per-image attention grid and the split-K small level: images

@@ -94,6 +94,10 @@ def test_conv_tile_options():
         with pytest.raises(rt.ItsdError):
             rt.set_option(key, val)
         rt.set_option(key, default)
+    for v in (0, 2, 1):  # 96-cout 8x8 tiles: off / always / auto (shipped)
+        rt.set_option("p4_c96", v)
+    with pytest.raises(rt.ItsdError):
+        rt.set_option("p4_c96", 3)
     rt.set_option("spin_bound", 0)  # diagnostic (fail-loud hand-off test), any bound >= 0
     rt.set_option("spin_bound", 1 << 22)
     with pytest.raises(rt.ItsdError):

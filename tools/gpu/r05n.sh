@@ -1,0 +1,17 @@
+set -o pipefail
+# round 5, run n: attn_block_kernel with every phase's weight stream issued ahead of the phase, vs the previous
+# build (m16all: the old attention); attention parity
+R=r05n
+mkdir -p gpurun_out/$R
+timeout -k 10 300 python -u -m pytest tests/test_gpu_attnblock.py tests/test_gpu_parity.py -k "attn or full_batch" -x -q --timeout 250 --timeout-method thread > gpurun_out/$R/tests.log 2>&1 || { echo tests_fail; grep -E "FAIL|Error|assert" gpurun_out/$R/tests.log | head -20; exit 1; }
+grep -E "passed|failed" gpurun_out/$R/tests.log | tail -2
+for r in 1 2; do
+  timeout -k 10 200 python tools/census.py --n 256 --reps 3 > gpurun_out/$R/census256_new_$r.txt 2>&1 || { echo census_fail; exit 1; }
+  timeout -k 10 200 python tools/census.py --n 256 --reps 3 --lib ab_libs/libitsd_hip_m16all.so > gpurun_out/$R/census256_old_$r.txt 2>&1 || { echo census_fail; exit 1; }
+done
+grep -H "attnblock  launches" gpurun_out/$R/census256_*.txt
+for r in 1 2; do
+  timeout -k 10 200 python tools/step_ab.py --n 256 --steps 30 --rounds 3 --variants base > gpurun_out/$R/step256_new_$r.txt 2>&1 || { echo ab_fail; exit 1; }
+  timeout -k 10 200 python tools/step_ab.py --n 32 --steps 30 --rounds 3 --variants base > gpurun_out/$R/step32_new_$r.txt 2>&1 || { echo ab_fail; exit 1; }
+done
+grep -H best gpurun_out/$R/step*.txt
