@@ -607,8 +607,8 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
   u->head_w = b.f32("head.weight", (int64_t)ch * 27);
   u->head_b = b.f32("head.bias", ch);
   u->head_out = b.act(H, H, ch);
-  if (u->bf16 && itsd::g_io_mfma && ch % 8 == 0 && ((H * H) % 128 == 0 || 128 % (H * H) == 0) &&
-      (H * H < 128 || 128 % H == 0)) {
+  // (head_mfma_kernel: 128-pixel tiles of whole rows, couts in 32-blocks; else the plain head kernel)
+  if (u->bf16 && itsd::g_io_mfma && ch % 32 == 0 && (H * H) % 128 == 0 && 128 % H == 0) {
     // [Cout][32] bf16, k = ci*9 + tap (the reference's flat per-cout order), zero-padded
     const float* hw = b.peek("head.weight", (int64_t)ch * 27);
     if (hw) {
@@ -863,7 +863,7 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     }
     a.zins = o.zins;
     a.dbg = itsd::g_conv_dbg;
-    a.xcd = itsd::g_p4_xcd;
+    a.xcd = itsd::g_p4_xcd == 1 || (itsd::g_p4_xcd == 2 && a.Wout == 8);
     if (o.subpix) {  // input-grid GEMM with 2x2 (upsample) / 3x3 (ConvTranspose2d) taps per phase (conv.hip)
       a.subpix = o.subpix;
       a.Hout = in.H; a.Wout = in.W;
@@ -1241,8 +1241,9 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_spin_bound = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "p4_xcd")) {  // conv3x3_gn_p4_kernel: deal each XCD a contiguous range of tiles (0 off, 1 on)
-    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p4_xcd in [0,1]");
+  if (!std::strcmp(key, "p4_xcd")) {  // conv3x3_gn_p4_kernel: deal each XCD a contiguous range of tiles (0 off, 1 on,
+                                       // 2 the 8x8 level only)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p4_xcd in [0,2]");
     itsd::g_p4_xcd = value;
     return ITSD_OK;
   }

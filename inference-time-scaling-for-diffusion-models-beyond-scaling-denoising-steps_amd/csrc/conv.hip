@@ -3196,7 +3196,8 @@ __global__ __launch_bounds__(256) void gn_coef_kernel(GNArgs g, float* coef) {
   {
     const int grp = tid >> 3, l8 = tid & 7;
     // the group's (channel, slot) items: its src1 channels x spi1 slots, then src2 x spi2 (with
-    // equal slot counts the order of a single spi, c = grp*gsz + k/spi)
+    // equal slot counts the order of a single spi, c = grp*gsz + k/spi). (Round 5: the same items in batches
+    // of 8 loads measured C4 +2.5 %, C3 +0.3 % step time -- profiles/r05/step_gn_batched_r05q.txt -- kept as is.)
     const int c0 = grp * gsz, nc1 = max(0, min(g.C1 - c0, gsz)), n1 = nc1 * spi1, n = n1 + (gsz - nc1) * spi2;
     double s = 0.0, q = 0.0;
     for (int k = l8; k < n; k += 8) {
@@ -3246,105 +3247,151 @@ hipError_t launch_gn_coef(const GNArgs& g, int n, float* coef, hipStream_t s) {
 // ---------------------------------------------------------------------------- head on MFMA
 // head = Conv2d(3, ch, 3, padding=1) (Model.py:219, ModelCondition.py:170) in bf16 mode as
 // an MFMA GEMM with K = 27 zero-padded to 32: D[cout][pixel] = W[cout][k] x patch[k][pixel],
-// k = ci*9 + ky*3 + kx. Block = 128 pixels (whole image rows, one GroupNorm statistics slot
-// or whole images) x 128 couts; the 3-channel input window sits in LDS as fp32, each lane
-// builds its pixel's two 8-element k-fragments from it; the shared epilogue adds the bias,
-// rounds, stores NHWC and writes the first GroupNorm's statistics slab.
-__global__ __launch_bounds__(256, 2) void head_mfma_kernel(HeadArgs h) {
-  __shared__ __attribute__((aligned(16))) char smem[EPI_BYTES];
+// k = ci*9 + ky*3 + kx. Block = 128 pixels (whole image rows: one GroupNorm statistics slot)
+// x 128 couts; the 3-channel input window sits in LDS as fp32. (Round 5) wave w owns couts
+// 32w .. 32w+31 over all 128 pixels (4 accumulators, one per 32-pixel block; each lane builds the
+// k-fragments of its pixel in every block from the window) and finishes in registers -- + bias, one
+// bf16 rounding, 16-B NHWC stores (permlane32 swap), the slot's statistics by lane butterflies -- so
+// the block needs 2.4 KB of LDS instead of the 67 KB fp32 output tile of the shared epilogue, and a CU
+// holds 4 blocks (register-bound, 121 VGPRs) instead of 2 (the launch is store- and latency-bound: 67 MB
+// of bf16 out at N = 256).
+__global__ __launch_bounds__(256, 4) void head_mfma_kernel(HeadArgs h) {
+  typedef bf16_t T;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const int HW = h.H * h.W, W = h.W;
   const long long tileP = (long long)blockIdx.x * 128;
   const int tileC = blockIdx.y * 128;
-  // input window: rows covering the tile's 128 pixels (+1 border), all images of the tile
+  // input window: the tile's 128 / W rows (+1 border) of its image
   const int img0 = (int)(tileP / HW), r0 = (int)(tileP - (long long)img0 * HW);
-  const int nimg = HW >= 128 ? 1 : 128 / HW;          // images per tile
-  const int rows = HW >= 128 ? 128 / W : h.H;         // output rows per image in the tile
-  const int y0 = r0 / W, TR = rows + 2, TW = W + 2;
-  float* tin = (float*)smem + 128 * 132;              // [nimg][3][TR][TW] behind the epilogue's E tile
-  // 4 window elements a thread per batch, all loads (from clamped addresses) issued before any use:
-  // one memory round trip for the 32 x 32 window (612 elements)
-  const int tot = nimg * 3 * TR * TW;
+  const int rows = 128 / W, y0 = r0 / W, TR = rows + 2, TW = W + 2;
+  __shared__ float tin[3 * 6 * 34 + 3 * 10 * 18];  // [3][TR][TW] (W = 32: 3 x 6 x 34; W <= 16 fits too)
+  const int tot = 3 * TR * TW;
   for (int i0 = tid; i0 < tot; i0 += 4 * 256) {
     float v[4];
     bool ok[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int i = i0 + 256 * u;
-      const int im = i / (3 * TR * TW), r = i - im * 3 * TR * TW;
-      const int ci = r / (TR * TW), q = r - ci * TR * TW, ty = q / TW, tx = q - ty * TW;
-      const int iy = y0 - 1 + ty, ix = tx - 1, img = img0 + im;
-      ok[u] = i < tot && img < h.n && iy >= 0 && iy < h.H && ix >= 0 && ix < W;
-      v[u] = h.x[ok[u] ? ((size_t)(img % h.x_img_mod) * 3 + ci) * HW + iy * W + ix : 0];
+      const int ci = i / (TR * TW), q = i - ci * TR * TW, ty = q / TW, tx = q - ty * TW;
+      const int iy = y0 - 1 + ty, ix = tx - 1;
+      ok[u] = i < tot && img0 < h.n && iy >= 0 && iy < h.H && ix >= 0 && ix < W;
+      v[u] = h.x[ok[u] ? ((size_t)(img0 % h.x_img_mod) * 3 + ci) * HW + iy * W + ix : 0];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (i0 + 256 * u < tot) tin[i0 + 256 * u] = ok[u] ? v[u] : 0.0f;
   }
-  // A fragments (weights) straight from the prepacked [Cout][32] bf16 matrix
-  bf16x8 af[4][2];
+  // A fragments (weights) of this wave's 32 couts straight from the prepacked [Cout][32] bf16 matrix
+  bf16x8 af[2];
+  {
+    const int co = tileC + wid * 32 + rl;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int co = tileC + mb * 32 + rl;
-      af[mb][s] = co < h.Cout ? *(const bf16x8*)(h.wmf + (size_t)co * 32 + 16 * s + 8 * hh)
-                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    for (int s2 = 0; s2 < 2; ++s2)
+      af[s2] = co < h.Cout ? *(const bf16x8*)(h.wmf + (size_t)co * 32 + 16 * s2 + 8 * hh) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
   __syncthreads();
-  // B fragment of this lane's pixel (column rl of wave wid's 32 pixels)
-  const int pl = wid * 32 + rl;
-  const int im = HW >= 128 ? 0 : pl / HW, pr = HW >= 128 ? pl : pl - im * HW;
-  const int ly = pr / W, lx = pr - ly * W;
-  bf16x8 bfr[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 16 * s + 8 * hh + j;
-      float v = 0.0f;
-      if (k < 27) {
-        const int ci = k / 9, tap = k - ci * 9, ky = tap / 3, kx = tap - ky * 3;
-        v = tin[((im * 3 + ci) * TR + ly + ky) * TW + lx + kx];
-      }
-      bfr[s][j] = (short)f2bf(v);
-    }
   f32x16 acc[4];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  for (int j = 0; j < 4; ++j) {
+    const int pl = j * 32 + rl, ly = pl / W, lx = pl - ly * W;
+    bf16x8 bfr[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[mb][r] = 0.f;
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) acc[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mb][s], bfr[s], acc[mb], 0, 0, 0);
+      for (int e = 0; e < 8; ++e) {
+        const int k = 16 * s2 + 8 * hh + e;
+        float v = 0.0f;
+        if (k < 27) {
+          const int ci = k / 9, tap = k - ci * 9, ky = tap / 3, kx = tap - ky * 3;
+          v = tin[(ci * TR + ly + ky) * TW + lx + kx];
+        }
+        bfr[s2][e] = (short)f2bf(v);
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s2], bfr[s2], acc[j], 0, 0, 0);
   }
-  __syncthreads();  // tin is dead; E[pixel][cout] overlays the front of smem
-  float* E = (float*)smem;
+  // epilogue: lane (rl, hh) holds pixel 32 j + rl, couts 32 w + 8 g + 4 hh + e (a wave past Cout: nothing)
+  const bool live = img0 < h.n && tileC + wid * 32 < h.Cout;
+  float s16[16], q16[16];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pl = j * 32 + rl;
+    uint32_t wv[4][2];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      f32x4 v4 = {acc[mb][4 * g], acc[mb][4 * g + 1], acc[mb][4 * g + 2], acc[mb][4 * g + 3]};
-      *(f32x4*)(E + pl * EROW + mb * 32 + 8 * g + 4 * hh) = v4;
+      const int c = tileC + wid * 32 + 8 * g + 4 * hh;
+      const f32x4 bb = *(const f32x4*)(h.b + c);
+      const T b0 = f2bf(acc[j][4 * g] + bb[0]), b1 = f2bf(acc[j][4 * g + 1] + bb[1]);
+      const T b2 = f2bf(acc[j][4 * g + 2] + bb[2]), b3 = f2bf(acc[j][4 * g + 3] + bb[3]);
+      wv[g][0] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+      wv[g][1] = (uint32_t)b2 | ((uint32_t)b3 << 16);
+      const float r0 = bf2f(b0), r1 = bf2f(b1), r2 = bf2f(b2), r3 = bf2f(b3);
+      s16[4 * g + 0] += r0; q16[4 * g + 0] = fmaf(r0, r0, q16[4 * g + 0]);
+      s16[4 * g + 1] += r1; q16[4 * g + 1] = fmaf(r1, r1, q16[4 * g + 1]);
+      s16[4 * g + 2] += r2; q16[4 * g + 2] = fmaf(r2, r2, q16[4 * g + 2]);
+      s16[4 * g + 3] += r3; q16[4 * g + 3] = fmaf(r3, r3, q16[4 * g + 3]);
     }
-  __syncthreads();
-  ConvArgs a{};
-  a.bias = h.b;
-  a.out = h.out;
-  a.Cout = h.Cout;
-  a.Hout = h.H; a.Wout = h.W;
-  a.M = h.n * HW;
-  a.stats = h.stats;
-  epilogue_from_E<bf16_t>(a, smem, (int)tileP, tileC, -1);
+#pragma unroll
+    for (int gp = 0; gp < 4; gp += 2) {
+      u32x4 o;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(wv[gp][d], wv[gp + 1][d], false, false);
+        o[d] = sw[0];
+        o[2 + d] = sw[1];
+      }
+      const int c8 = tileC + wid * 32 + 8 * (gp + hh);
+      if (live) *(u32x4*)((T*)h.out + (size_t)(tileP + pl) * h.Cout + c8) = o;
+    }
+  }
+  if (h.stats && live) {  // the tile's 128 pixels = one slot: 32 values a lane -> one (p5's W >= 16 butterfly)
+    float v[32];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      v[e] = s16[e];
+      v[16 + e] = q16[e];
+    }
+    auto xchg = [](float x, auto wc) {
+      constexpr int w = decltype(wc)::value;
+      const int xi = __builtin_bit_cast(int, x);
+      int r;
+      if constexpr (w == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+      else if constexpr (w == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+      else if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+      else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (w << 10));
+      return __builtin_bit_cast(float, r);
+    };
+    auto halve = [&](auto wc) {
+      constexpr int d = decltype(wc)::value;
+      const bool up = (rl & d) != 0;
+#pragma unroll
+      for (int ii = 0; ii < d; ++ii) {
+        const float lo = v[ii], hi = v[ii + d];
+        v[ii] = (up ? hi : lo) + xchg(up ? lo : hi, wc);
+      }
+    };
+    halve(std::integral_constant<int, 16>{});
+    halve(std::integral_constant<int, 8>{});
+    halve(std::integral_constant<int, 4>{});
+    halve(std::integral_constant<int, 2>{});
+    halve(std::integral_constant<int, 1>{});
+    const long long slot = tileP / 128;
+    const int e = rl & 15, co = wid * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+    h.stats[(slot * 2 + (rl >> 4)) * h.Cout + tileC + co] = v[0];
+  }
 }
 
 hipError_t launch_head_mfma(const HeadArgs& h, hipStream_t s) {
   const int HW = h.H * h.W;
-  const int nimg = HW >= 128 ? 1 : 128 / HW, rows = HW >= 128 ? 128 / h.W : h.H;
-  if (!h.wmf || (HW % 128 && 128 % HW) || (HW >= 128 && 128 % h.W) || h.Cout % 8 ||
-      (size_t)(128 * 132 + nimg * 3 * (rows + 2) * (h.W + 2)) * 4 > (size_t)EPI_BYTES)
+  // (128-pixel tiles of whole rows: one statistics slot each; the window fits tin)
+  if (!h.wmf || HW % 128 || 128 % h.W || h.Cout % 32 || 3 * (128 / h.W + 2) * (h.W + 2) > 3 * 6 * 34 + 3 * 10 * 18)
     return hipErrorInvalidValue;
   ITSD_LAUNCH(head_mfma_kernel, dim3((unsigned)(((long long)h.n * HW + 127) / 128), (h.Cout + 127) / 128), dim3(256), 0,
-                     s, h);
+              s, h);
   return hipGetLastError();
 }
 

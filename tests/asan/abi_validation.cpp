@@ -70,7 +70,7 @@ int main() {
   expect("set_option conv_variant=2 (default)", itsd_set_option("conv_variant", 2), ITSD_OK);
   expect("set_option spin_bound=-1", itsd_set_option("spin_bound", -1), ITSD_ERR_INVALID);
   expect("set_option spin_bound=4194304 (default)", itsd_set_option("spin_bound", 1 << 22), ITSD_OK);
-  expect("set_option p4_xcd=2", itsd_set_option("p4_xcd", 2), ITSD_ERR_INVALID);
+  expect("set_option p4_xcd=3", itsd_set_option("p4_xcd", 3), ITSD_ERR_INVALID);
   expect("set_option attn_aq=48", itsd_set_option("attn_aq", 48), ITSD_ERR_INVALID);
   expect("set_option p4_w=8 (64x64 removed)", itsd_set_option("p4_w", 8), ITSD_ERR_INVALID);
   expect("set_option convt_prune=2", itsd_set_option("convt_prune", 2), ITSD_ERR_INVALID);
