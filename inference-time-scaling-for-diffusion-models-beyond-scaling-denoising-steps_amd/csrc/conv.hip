@@ -57,7 +57,10 @@ int g_small_minks = 8;    // conv_small split K: >= this many K-chunks a slice (
                           // 2: N=32 step -2.3 %, N=64 -0.9 %, N=256 / C3 / C4 equal, profiles/r04/small_minks_ab.txt)
 int g_convt_prune = 1;    // ConvTranspose2d sub-pixel phases skip their all-zero taps (itsd_set_option "convt_prune")
 int g_subpix_split = 1;   // under-filled sub-pixel conv_pipe launches split K in-launch (itsd_set_option "subpix_split")
-int g_p4_xcd = 0;        // conv3x3_gn_p4_kernel: each XCD a contiguous range of tiles (ConvArgs::xcd)
+int g_p4_xcd = 2;        // conv3x3_gn_p4_kernel: each XCD a contiguous range of tiles (ConvArgs::xcd): 0 off, 1 every
+                         // level (measured -2 % at N = 256), 2 the 8x8 level only (a pixel tile's cout tiles on one
+                         // XCD: its input read once per L2; 8x8 HBM traffic 98.5 -> 65.1 MB a launch at equal step
+                         // time, profiles/r05/p4_xcd8_traffic_r05s.txt)
 int g_p4_c96 = 1;        // 8x8 p4 on 96-cout tiles where they fill the CUs better: 0 off, 1 auto, 2 always (conv_p4_c96)
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
@@ -3606,8 +3609,10 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // for K >= 7168: the CFG's merged 5x5 DownSample into 8x8, K = 12800 at 2N = 64, measured 156 us on
     // conv_small's 64x64 tiles vs 97 us on the 128-tile pipe, profiles/r04/census_archC_2N64_small8_k.txt)
     const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
-    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256 &&
-                        a.K < 7168;
+    const unsigned tiles128 = grid.x * grid.y, G128 = (unsigned)g_num_cus;
+    const bool part_round = tiles128 % G128 && tiles128 % G128 < G128 * 3 / 4 && tiles128 < 4 * G128;
+    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B &&
+                        (tiles128 < G128 || (g_small_8x8 == 2 && part_round)) && a.K < 7168;
     if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
         (a.Hout * a.Wout <= 16 || wide || small8) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
