@@ -1179,9 +1179,8 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_conv1x1 = value;
     return ITSD_OK;
   }
-  if (!std::strcmp(key, "small_8x8")) {  // conv_small (split K) for under-filled 8x8-level convs (2: also where the
-                                         // 128-tile grid's last round is part-empty)
-    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "small_8x8 in [0,2]");
+  if (!std::strcmp(key, "small_8x8")) {  // conv_small (split K) for under-filled 8x8-level convs
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_8x8 in [0,1]");
     itsd::g_small_8x8 = value;
     return ITSD_OK;
   }

@@ -3609,10 +3609,10 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
     // for K >= 7168: the CFG's merged 5x5 DownSample into 8x8, K = 12800 at 2N = 64, measured 156 us on
     // conv_small's 64x64 tiles vs 97 us on the 128-tile pipe, profiles/r04/census_archC_2N64_small8_k.txt)
     const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
-    const unsigned tiles128 = grid.x * grid.y, G128 = (unsigned)g_num_cus;
-    const bool part_round = tiles128 % G128 && tiles128 % G128 < G128 * 3 / 4 && tiles128 < 4 * G128;
-    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B &&
-                        (tiles128 < G128 || (g_small_8x8 == 2 && part_round)) && a.K < 7168;
+    // (round 5: also where the 128-tile grid's last round is part-empty -- N = 256's 8x8 shortcuts, 384 tiles --
+    // measured 31 -> 48 us a launch, N = 256 step +0.8 %, profiles/r05/small8_part_round_r05t.txt: not taken)
+    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256 &&
+                        a.K < 7168;
     if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
         (a.Hout * a.Wout <= 16 || wide || small8) &&
         gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
