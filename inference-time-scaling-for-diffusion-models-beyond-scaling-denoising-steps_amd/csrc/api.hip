@@ -34,6 +34,7 @@ hipError_t launch_attn_block(const AttnBlockArgs&, int, hipStream_t);
 int g_attn_fuse = 1;  // fused AttnBlock kernel at S = 64 (Arch A's 8x8 level): 0 off, 1 on (itsd_set_option "attn_fuse", read at create)
 int g_tap_prune = 1;   // drop conv taps that read only padding for every output pixel ("tap_prune", read at create)
 int g_down_merge = 1;  // CFG DownSample c1 (3x3) + c2 (5x5) as one 5x5 conv ("down_merge", read at create)
+int g_attn_s1 = 1;    // one-token AttnBlock (the CFG 1x1 level) as GroupNorm + one folded 1x1 conv ("attn_s1", read at create)
 template <typename T> hipError_t launch_head(const HeadArgs&, hipStream_t);
 template <typename T> hipError_t launch_tail(const TailArgs&, hipStream_t);
 hipError_t launch_emb_input(const int*, int, const float*, const float*, int, float*, int, hipStream_t);
@@ -517,6 +518,40 @@ struct Builder {
     if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
     if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
     else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
+    if (attn && H * W == 1 && itsd::g_attn_s1) {
+      // AttnBlock over ONE token (ModelCondition.py's 1x1 level; Model.py:145-164): the softmax over a single key
+      // is exp(0) / exp(0) = 1 exactly, so h = v and the block is x + proj(v(GN(x))) = x + Wf GN(x) + bf with
+      // Wf = Wp Wv, bf = Wp bv + bp (folded here in fp64): one GroupNorm and one 1x1 conv instead of GroupNorm,
+      // the q|k|v conv, the attention kernel and the proj conv (q and k never reach the output)
+      const std::string a = p + ".attn";
+      const int64_t cc = (int64_t)out_ch * out_ch;
+      const float* wv = get(a + ".proj_v.weight", cc);
+      const float* bv = get(a + ".proj_v.bias", out_ch);
+      const float* wp = get(a + ".proj.weight", cc);
+      const float* bp = get(a + ".proj.bias", out_ch);
+      // (q / k: validated and counted as the reference's keys, never read)
+      const bool qk = get(a + ".proj_q.weight", cc) && get(a + ".proj_q.bias", out_ch) && get(a + ".proj_k.weight", cc) &&
+                      get(a + ".proj_k.bias", out_ch);
+      if (wv && bv && wp && bp && qk) {
+        std::vector<float> wf((size_t)cc), bf((size_t)out_ch);
+        std::vector<double> row((size_t)out_ch);
+        for (int oc = 0; oc < out_ch; ++oc) {
+          std::fill(row.begin(), row.end(), 0.0);
+          double bacc = (double)bp[oc];
+          for (int c = 0; c < out_ch; ++c) {
+            const double w = (double)wp[(size_t)oc * out_ch + c];
+            const float* vr = wv + (size_t)c * out_ch;
+            for (int ic = 0; ic < out_ch; ++ic) row[ic] += w * (double)vr[ic];
+            bacc += w * (double)bv[c];
+          }
+          for (int ic = 0; ic < out_ch; ++ic) wf[(size_t)oc * out_ch + ic] = (float)row[ic];
+          bf[oc] = (float)bacc;
+        }
+        int ga = act(H, W, out_ch);
+        gn(o, -1, ga, a + ".group_norm", out_ch, 0);
+        return conv_layer(ga, -1, a + ".proj", out_ch, 1, 1, 0, 0, H, W, -1, o, "", wf.data(), bf.data());
+      }
+    }
     if (attn && u->bf16 && itsd::g_attn_fuse && attn_block_ok(H * W, out_ch)) {
       // the whole AttnBlock in one launch (kernels.hip attn_block_kernel)
       const std::string a = p + ".attn";
@@ -1313,6 +1348,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "attn_wide")) {  // channel-split attention (attn_cs_kernel): 0 off, 1 auto (C >= 384 at S >= 256; C = 1024), 2 wherever it applies
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "attn_wide in [0,2]");
     itsd::g_attn_wide = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "attn_s1")) {  // one-token AttnBlock folded to GroupNorm + one 1x1 conv (UNets created afterwards)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "attn_s1 in [0,1]");
+    itsd::g_attn_s1 = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "attn_fuse")) {  // fused AttnBlock kernel (S = 64): 0 off, 1 on (UNets created afterwards)

@@ -662,6 +662,39 @@ def test_p4_96_cout_tiles_bit_identical_n256():
     assert _rel_l2(c96[idx], ref) < REL_L2_BF16
 
 
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 1e-2)])
+def test_one_token_attnblock_fold_archC(precision, tol):
+    """Arch C's 1x1-level AttnBlocks (ModelCondition.py, one token): the softmax over a single key is exactly 1,
+    so the block is x + proj(v(GN(x))); the build folds proj and v into one 1x1 conv (Wp Wv, Wp bv + bp in fp64)
+    behind the GroupNorm (option attn_s1, read at create). Against the four-op path (attn_s1 = 0) on the same
+    guided batch: relative L2 <= 1e-5 in fp32 (a reassociation of the two products), <= 1e-2 in bf16 (one bf16
+    rounding of v fewer); and the folded forward against the oracle."""
+    a = ARCH_C
+    gen = torch.Generator().manual_seed(77)
+    n = 8
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    lab = torch.arange(n) % 11
+    outs = {}
+    for v in (1, 0):
+        rt.set_option("attn_s1", v)  # (read when the native UNet is built: at its first forward)
+        try:
+            net = _net(a, precision)
+            outs[v] = net(x.cuda(), t.cuda(), lab.cuda()).float().cpu()
+        finally:
+            rt.set_option("attn_s1", 1)
+        del net
+        torch.cuda.empty_cache()
+    assert not torch.equal(outs[1], outs[0])  # (the two builds differ: the fold took effect)
+    d = _rel_l2(outs[1], outs[0])
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[:2], t[:2], lab[:2])
+    e = _rel_l2(outs[1][:2], ref)
+    print(f"Arch C {precision}: folded one-token AttnBlocks vs four-op path rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d <= tol
+    assert e <= (1e-4 if precision == "fp32" else REL_L2_BF16)
+
+
 def test_forward_bf16_full_batch_vs_oracle_subset():
     """The bench batch (N=256) runs the persistent fused convs with several tiles per block
     (4 at 32x32, 2 at 16x16), the 2-blocks-per-image attention grid and the split-K small level: images

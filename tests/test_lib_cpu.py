@@ -90,7 +90,7 @@ def test_conv_tile_options():
     for key, val in (("conv_wide", 0), ("gn_reg", 4), ("tail_px", 64), ("p4_m16", 1), ("small_korder", 1)):
         with pytest.raises(rt.ItsdError, match="unknown option"):
             rt.set_option(key, val)
-    for key, val, default in (("attn_fuse", 2, 1), ("p4_w", 15, 7), ("conv_variant", 3, 2), ("conv_variant", 0, 2)):
+    for key, val, default in (("attn_fuse", 2, 1), ("attn_s1", 2, 1), ("p4_w", 15, 7), ("conv_variant", 3, 2), ("conv_variant", 0, 2)):
         with pytest.raises(rt.ItsdError):
             rt.set_option(key, val)
         rt.set_option(key, default)
