@@ -1804,9 +1804,13 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 // (HBM latency once per batch, not per chunk). Each wave owns 2 x 16 pixels:
 // eps[pixel][co] = sum_k patch[pixel][k] W[co][k] on v_mfma_f32_16x16x32_bf16
 // (k = tap*C + ci; 9C/32 k-steps; B columns 3..15 are zero).
-// TM_PX output pixels per block: 128 (64 -- a smaller halo, 3 blocks a CU -- measured +0.3 %, removed in round 5)
-template <int TM_PX>
-__global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
+// TM_PX output pixels per block: 128 (64 -- a smaller halo, 3 blocks a CU -- measured +0.3 %, removed in round 5);
+// NTH threads: 512 (round 5: 8 waves, one 16-pixel group each -- twice the waves a CU for the halo transform's
+// latency: 71.1 -> 65.5 us a launch at N = 256 against 256 threads, profiles/r05/tail_512_vs_256_r05x.txt)
+template <int TM_PX, int NTH>
+__global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
+  constexpr int NW = NTH / 64, GPW = TM_PX / 16 / NW;  // waves; 16-pixel MFMA groups a wave
+  static_assert(GPW >= 1 && GPW * 16 * NW == TM_PX, "tail geometry");
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   const int C = a.C, W = a.W, H = a.H, HW = H * W;
   const int rpb = TM_PX / W, bpi = H / rpb, PST = 2 * C + 16, NKS = 9 * C / 32;
@@ -1817,17 +1821,17 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
   float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);     // [2 passes][TM_PX][3]
   float* cfl = red + 2 * TM_PX * 3;                            // [C/8][16] this pass's GN coefficients
   const int m = lane & 15, kg = lane >> 4;
-  int hbase[2];
+  int hbase[GPW];
 #pragma unroll
-  for (int gi = 0; gi < 2; ++gi) {
-    const int pl = wid * 32 + gi * 16 + m, py = pl / W, px = pl - py * W;
+  for (int gi = 0; gi < GPW; ++gi) {
+    const int pl = wid * 16 * GPW + gi * 16 + m, py = pl / W, px = pl - py * W;
     hbase[gi] = (py * (W + 2) + px) * PST + 16 * kg;
   }
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int cpp = C / 8, npx = (rpb + 2) * (W + 2), total = npx * cpp;
-  // the sampler step's operands of this thread's output items (it = tid, tid + 256), loaded now: their
+  // the sampler step's operands of this thread's output items (it = tid, tid + NTH, ..), loaded now: their
   // latency hides behind the halo staging and the MFMAs
-  constexpr int TIT = (TM_PX * 3 + 255) / 256;
+  constexpr int TIT = (TM_PX * 3 + NTH - 1) / NTH;
   float xpre[TIT];
   int tpre = 0;
   float c1pre = 0.f, c2pre = 0.f, svpre = 0.f;
@@ -1844,22 +1848,22 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     svpre = a.sqrt_var[tpre];
 #pragma unroll
     for (int k = 0; k < TIT; ++k) {
-      const int it = tid + 256 * k, opx = it < TM_PX * 3 ? it / 3 : 0, oc = it < TM_PX * 3 ? it - opx * 3 : 0;
+      const int it = tid + NTH * k, opx = it < TM_PX * 3 ? it / 3 : 0, oc = it < TM_PX * 3 ? it - opx * 3 : 0;
       const int rem = (y0 + opx / W) * W + (opx - (opx / W) * W);
       xpre[k] = a.x[((size_t)img * 3 + oc) * HW + rem];
     }
   }
-  constexpr int TB = 16;  // halo items a thread per batch (C = 128, 32 x 32: the whole halo in one batch)
+  constexpr int TB = 4096 / NTH;  // halo items a thread per batch (C = 128, 32 x 32: the whole halo in one batch)
   for (int pass = 0; pass < (a.cfg ? 2 : 1); ++pass) {
     const int im = img + pass * a.n;
     __syncthreads();
     const bf16_t* gb = (const bf16_t*)a.g + (size_t)im * HW * C;
-    for (int i0 = 0; i0 < total; i0 += TB * 256) {
+    for (int i0 = 0; i0 < total; i0 += TB * NTH) {
       u32x4 v[TB];
       int dst[TB];
 #pragma unroll
       for (int u = 0; u < TB; ++u) {  // all loads of the batch first
-        const int i = i0 + u * 256 + tid;
+        const int i = i0 + u * NTH + tid;
         const int hp = i / cpp, ch = i - hp * cpp;
         const int hy = hp / (W + 2), hx = hp - hy * (W + 2);
         const int gy = y0 - 1 + hy, gx = hx - 1;
@@ -1870,9 +1874,9 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
       }
       if (i0 == 0) {  // the image's GroupNorm coefficients (and, first pass, the weights) into LDS, their
                       // loads behind the batch's: one memory round trip for all of them
-        for (int i = tid; i < cpp * 16; i += 256) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
+        for (int i = tid; i < cpp * 16; i += NTH) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
         if (pass == 0)
-          for (int i = tid; i < NKS * 12; i += 256) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
+          for (int i = tid; i < NKS * 12; i += NTH) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
         __syncthreads();
       }
 #pragma unroll
@@ -1900,9 +1904,11 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
       }
     }
     __syncthreads();
-    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[GPW];
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) acc[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int cpt = C / 32;
-    if (wid * 32 < TM_PX) {  // (TM_PX = 64: waves 0, 1 own the block's pixels)
+    {
 #pragma unroll 4
     for (int ks = 0; ks < NKS; ++ks) {
       const int tap = ks / cpt, ci0 = (ks - tap * cpt) * 32;
@@ -1910,7 +1916,7 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
       const int toff = (ky * (W + 2) + kx) * PST + ci0 * 2;
       const bf16x8 bw = m < 3 ? wl[(ks * 4 + kg) * 3 + m] : z8;
 #pragma unroll
-      for (int gi = 0; gi < 2; ++gi) {
+      for (int gi = 0; gi < GPW; ++gi) {
         const bf16x8 af = *(const bf16x8*)(halo + hbase[gi] + toff);
         acc[gi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[gi], 0, 0, 0);
       }
@@ -1918,16 +1924,16 @@ __global__ __launch_bounds__(256, 2) void tail_mfma_kernel(TailArgs a) {
     // D[pixel 4*kg + i][co = m] of this wave's two 16-pixel groups
     if (m < 3) {
 #pragma unroll
-      for (int gi = 0; gi < 2; ++gi)
+      for (int gi = 0; gi < GPW; ++gi)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[(pass * TM_PX + wid * 32 + gi * 16 + 4 * kg + i) * 3 + m] = acc[gi][i];
+        for (int i = 0; i < 4; ++i) red[(pass * TM_PX + wid * 16 * GPW + gi * 16 + 4 * kg + i) * 3 + m] = acc[gi][i];
     }
     }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < TIT; ++k) {
-    const int it = tid + 256 * k;
+    const int it = tid + NTH * k;
     if (it >= TM_PX * 3) break;
     const int opx = it / 3, oc = it - opx * 3;
     float e = red[opx * 3 + oc] + a.b[oc];
@@ -1975,14 +1981,14 @@ hipError_t launch_tail_mfma(const TailArgs& a, hipStream_t s) {
   if (!a.coef || !a.wmf || !tail_mfma_ok(a.H, a.W, a.C)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)tail_mfma_kernel<128>}) {
+    for (const void* f : {(const void*)tail_mfma_kernel<128, 512>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
-  ITSD_LAUNCH(tail_mfma_kernel<128>, dim3(a.n * (a.H / (128 / a.W))), dim3(256), tail_mfma_smem_px(128, a.H, a.W, a.C),
-              s, a);
+  ITSD_LAUNCH((tail_mfma_kernel<128, 512>), dim3(a.n * (a.H / (128 / a.W))), dim3(512),
+              tail_mfma_smem_px(128, a.H, a.W, a.C), s, a);
   return hipGetLastError();
 }
 
