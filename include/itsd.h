@@ -179,7 +179,7 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
 
 /* Process-wide switches for A/B measurements (api.hip lists every key): kernel variants and
  * tile choices ("conv_variant", "splitk", "small_conv", "gn_wide", "fuse_gn", "io_mfma",
- * "p4_sub", "p4_plain", "p5", "p5_split", "gn_fold", "attn_split", "attn_wide", "attn_wide_nq",
+ * "p4_sub", "p4_plain", "p5", "p5_split", "p5_sc", "gn_fold", "attn_split", "attn_wide", "attn_wide_nq",
  * "conv1x1", "small_wide", "small_8x8", "subpix_split", "convt_prune", "small_minks"; build-time, read at create: "attn_fuse",
  * "tap_prune", "down_merge") and measurement-only ablations ("conv_dbg"). Defaults are the shipped
  * choices; every alternative is covered by a parity test. */

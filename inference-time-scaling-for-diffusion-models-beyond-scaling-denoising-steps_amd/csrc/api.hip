@@ -49,6 +49,7 @@ bool conv_gn_eligible(int H, int W);
 bool p5_eligible(int H, int W);
 bool conv_p5_selected(const ConvArgs& a);
 bool conv_p4_selected(const ConvArgs& a);
+bool conv_p5_sc_fold(const ConvArgs& a);
 int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
@@ -132,6 +133,10 @@ struct Op {
   size_t coef = SIZE_MAX;    // GNCOEF: output; CONV: GroupNorm+SiLU coefficients of the input (fused conv)
   size_t wt2 = 0, bias2 = 0;  // ATTNBLOCK: the proj matrix (fragment-packed) and bias; wt / bias: q|k|v
   size_t gn_gamma = SIZE_MAX, gn_beta = SIZE_MAX;  // CONV with coef: its input GroupNorm's affine (gn_fold)
+  // a ResBlock's block2 conv and its 1x1 shortcut (conv3x3_gn_p5_kernel folds the shortcut in as K slices, ConvArgs
+  // sc_*): on block2, the shortcut op, its weights in fragment order and the two biases summed; on the shortcut, block2
+  int sc_op = -1, sc_into = -1;
+  size_t sc_wfrag = SIZE_MAX, bias_sc = SIZE_MAX;
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -515,9 +520,28 @@ struct Builder {
       g2 = act(H, W, out_ch);
       gn(h1, -1, g2, p + ".block2.0", out_ch, 1);
     }
-    if (in_ch != out_ch) resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
+    int isc = -1;
+    if (in_ch != out_ch) {
+      resid = conv_layer(x1, x2, p + ".shortcut", out_ch, 1, 1, 0, 0, H, W);
+      isc = (int)u->ops.size() - 1;
+    }
     if (f2) o = conv_layer(h1, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid, p + ".block2.0");
     else o = conv_layer(g2, -1, p + ".block2.3", out_ch, 3, 1, 1, 0, H, W, -1, resid);
+    if (f2 && isc >= 0 && u->bf16 && out_ch % 32 == 0 && u->acts[x1].C % 64 == 0 && (x2 < 0 || u->acts[x2].C % 64 == 0)) {
+      // the shortcut as extra K slices of block2 where block2 runs on conv3x3_gn_p5_kernel (run time: conv_args)
+      const float* wsc = peek(p + ".shortcut.weight", (int64_t)out_ch * in_ch);
+      const float* bsc = peek(p + ".shortcut.bias", out_ch);
+      const float* bb2 = peek(p + ".block2.3.bias", out_ch);
+      if (wsc && bsc && bb2) {
+        std::vector<float> bs((size_t)out_ch);
+        for (int c = 0; c < out_ch; ++c) bs[c] = bb2[c] + bsc[c];
+        Op& c2 = u->ops.back();
+        c2.sc_wfrag = pack_frag(wsc, out_ch, in_ch, 1);
+        c2.bias_sc = ar.add(bs.data(), (size_t)out_ch * 4);
+        c2.sc_op = isc;
+        u->ops[isc].sc_into = (int)u->ops.size() - 1;
+      }
+    }
     if (attn && H * W == 1 && itsd::g_attn_s1) {
       // AttnBlock over ONE token (ModelCondition.py's 1x1 level; Model.py:145-164): the softmax over a single key
       // is exp(0) / exp(0) = 1 exactly, so h = v and the block is x + proj(v(GN(x))) = x + Wf GN(x) + bf with
@@ -932,6 +956,20 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     a.gn_gamma = u->wp(o.gn_gamma);
     a.gn_beta = u->wp(o.gn_beta);
   }
+  if (o.sc_op >= 0 && itsd::g_p5_sc) {  // the shortcut folded in (run_program then skips the shortcut's launch)
+    const Op& sc = u->ops[o.sc_op];
+    ConvArgs t = a;
+    t.sc_src1 = u->ap(sc.src1);
+    t.sc_src2 = sc.src2 >= 0 ? u->ap(sc.src2) : nullptr;
+    t.sc_C1 = u->acts[sc.src1].C;
+    t.sc_C2 = sc.src2 >= 0 ? u->acts[sc.src2].C : 0;
+    t.sc_wfrag = u->wdev + o.sc_wfrag;
+    if (conv_p5_sc_fold(t)) {
+      a = t;
+      a.bias = u->wp(o.bias_sc);
+      a.resid = nullptr;
+    }
+  }
   return ITSD_OK;
 }
 
@@ -1068,6 +1106,10 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     if (o.kind == OP_GNCOEF && oi + 1 < u->ops.size() && u->ops[oi + 1].kind == OP_CONV) {
       ConvArgs na{};  // gn_fold: the consumer conv finalizes this GroupNorm itself
       if (conv_args(u, u->ops[oi + 1], c, na) == ITSD_OK && na.gn_fold) continue;
+    }
+    if (o.kind == OP_CONV && o.sc_into >= 0) {
+      ConvArgs na{};  // a shortcut its block2 conv runs as K slices
+      if (conv_args(u, u->ops[o.sc_into], c, na) == ITSD_OK && na.sc_C1 + na.sc_C2 > 0) continue;
     }
     int kind = o.kind == OP_ATTNBLOCK ? kCensusAttnBlock : (int)o.kind;
     cur_op = (int)oi + 1;
@@ -1320,6 +1362,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p5_split")) {  // its K slices: 0 auto (cost model), 1..16 forced
     if (value < 0 || value > 16) return fail(ITSD_ERR_INVALID, "p5_split in [0,16]");
     itsd::g_p5_split = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p5_sc")) {  // ResBlock 1x1 shortcuts as K slices of their block2 p5 conv: 0 off, 1 auto, 2 always
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_sc in [0,2]");
+    itsd::g_p5_sc = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p4 / p5_kernel: 0 off, 1 on

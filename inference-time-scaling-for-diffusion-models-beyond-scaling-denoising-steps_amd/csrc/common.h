@@ -30,6 +30,7 @@ extern int g_p4_c96;        // 8x8 conv3x3_gn_p4_kernel<8, 512> (96-cout tiles):
 extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel<W, 128>: 0 off, 1 on (itsd_set_option "p4_sub")
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
+extern int g_p5_sc;         // 1x1 shortcut folded into the block2 p5 conv: 0 off, 1 auto, 2 always ("p5_sc")
 extern int g_spin_bound;     // polls before an in-kernel hand-off wait fails: ITSD_ERR_HANDOFF ("spin_bound", diagnostic)
 extern int g_attn_split;     // attn_block_split_kernel at small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
@@ -159,6 +160,14 @@ struct ConvArgs {
   int gn_spi1, gn_spi2;
   const float* gn_gamma;
   const float* gn_beta;
+  // conv3x3_gn_p5_kernel with the ResBlock's 1x1 shortcut folded in (Model.py:200-205, h + shortcut(x)):
+  // sc_split more K slices after the ksplit 3x3 ones, over x = sc_src1 ++ sc_src2 (raw, no GroupNorm) with the
+  // shortcut's fragment-ordered weights sc_wfrag [Cout/32][(sc_C1+sc_C2)/16][64][8]; bias = both biases summed,
+  // resid = null. sc_split == 0: no shortcut slices
+  const void* sc_src1;
+  const void* sc_src2;
+  int sc_C1, sc_C2, sc_split;
+  const void* sc_wfrag;
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -65,6 +65,7 @@ int g_p4_c96 = 1;        // 8x8 p4 on 96-cout tiles where they fill the CUs bett
 int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's sub-pixel form (AB = 128)
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
+int g_p5_sc = 1;         // the ResBlock's 1x1 shortcut folded into its block2 p5 conv: 0 off, 1 auto (cost model), 2 always
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -1443,6 +1444,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #ifndef ITSD_P4_M16
 #define ITSD_P4_M16 2
 #endif
+#ifndef ITSD_P4_HSWZ
+#define ITSD_P4_HSWZ 1  // the 16x16x32 forms' halo swizzle h & 6 (0: (h >> 1) & 7, as the 32x32x16 forms; A/B builds)
+#endif
 constexpr int P4_RING = 6;  // A k-step slots (prefetch distance 5 k-steps = 40 MFMAs); divides the 36 k-steps
                             // of a chunk, so the slots of the next chunk's prefetched steps line up
 constexpr int P4_BD = 2;    // B fragment buffers (reads P4_BD - 1 k-steps = 8 MFMAs ahead)
@@ -1479,6 +1483,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // (COMPACT + M16: a second zero row 64 rows past the first, so that a lane pointed at the zero row reads zeros at
   // the +64-row immediate offset of its pixel blocks 4..7 too)
   constexpr int ZROWS = COMPACT ? (M16 ? 65 : 1) : 0;
+  // halo row h's 16-B units are stored XOR-permuted by hswz(h). ds_read_b128 serves a wave in four 16-lane groups
+  // ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, +32: MI355X_MICROARCH.md, LDS) over 16 slots of 16 B (row parity x
+  // unit). The 32x32x16 B reads (lane = 32 rows x 2 halves) are conflict-free for any tap offset with
+  // (h >> 1) & 7; the 16x16x32 ones (lane = 16 rows x 4 k-groups: a group holds rows +0-3 / +12-15 of one k-group
+  // and +4-11 of the other) were 2-way at 3 of every 4 row offsets with it (the round-5 7x rise of
+  // SQ_LDS_BANK_CONFLICT, profiles/r05/p4_lds_conflicts_r05ab.txt), and are conflict-free at every offset with
+  // h & 6 (exhaustive check over offsets, groups and both half-steps: tools/halo_swizzle.py)
+  auto hswz = [](int h) { return M16 && ITSD_P4_HSWZ ? (h & 6) : ((h >> 1) & 7); };
   // C96 (AB bit 512, 8x8 only): 96-cout tiles -- Cout = 384 gives 4 cout tiles, so N = 256's 64 pixel tiles make
   // 256 tiles for the 256 CUs instead of 192 with 128 couts (a quarter of the chip idle). Each MFMA wave holds 48
   // couts (3 16x16 blocks); the LDS output tile keeps its 64-cout halves (48 used: units 0..5 of 8)
@@ -1688,10 +1700,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
         int tb[4];
         int zad = 0;  // (W = 16: this lane's zero-row address, for the two pixel blocks a wave-uniform tap row leaves)
         bf16x8 fb[BD][4];
-        // B unit u = (k32-step u >> 1, pixel blocks 4 (u & 1) .. +3): byte (h * 128 + ((kg ^ sw(h)) << 4)) ^ (s2 << 6),
+        // B unit u = (k32-step u >> 1, pixel blocks 4 (u & 1) .. +3): byte (h * 128 + ((kg ^ hswz(h)) << 4)) ^ (s2 << 6),
         // s2 = the step's half of the tap's 64 channels. Four address registers a tap, rebuilt at its first unit:
         // a pixel block 16 rows (32x32: block 2t + 1 of block 2t) or 64 rows (COMPACT: block j + 4 of block j) on has
-        // the same swizzle (sw = (h >> 1) & 7), so it is an immediate offset (2048 / 8192 B) of its partner's address.
+        // the same swizzle (hswz has period 8 rows), so it is an immediate offset (2048 / 8192 B) of its partner's address.
         // COMPACT: a tap reading outside its image reads a zero row (x: per lane, all blocks -- the zero rows 256 and
         // 320; y at 16x16: rows -1 / 16 are wave-uniform, block 0 at ky = 0 of wave row 0, block 7 at ky = 2 of wave
         // row 1 -- those two reads take the zero-row address; their partners are in range)
@@ -1713,10 +1725,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
               } else {
                 h = p0 + t * W2 + ky * W2 + kx;  // block 2t
               }
-              tb[t] = hoff + h * ROWB + ((kg ^ ((h >> 1) & 7)) << 4);
+              if constexpr (COMPACT) tb[t] = hoff + h * ROWB + ((kg ^ hswz(h)) << 4);
+              else tb[t] = (hoff + h * ROWB + (hswz(h) << 4)) ^ (kg << 4);  // (the same bits; fewer registers at 32x32)
             }
             if constexpr (COMPACT && W == 16)
-              if (ky != 1) zad = hoff + ZROW * ROWB + ((kg ^ ((ZROW >> 1) & 7)) << 4);
+              if (ky != 1) zad = hoff + ZROW * ROWB + ((kg ^ hswz(ZROW)) << 4);
           }
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
@@ -2180,8 +2193,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   if (a.dbg & (1 << 21)) __builtin_amdgcn_s_setprio(2);
   const int dump = NSEG * HS * ROWB + (lch << 4);  // (not COMPACT: the scratch rows' write target)
   const int hrow0 = (COMPACT ? sg * HWs : sg * HS) + (lt >> 3), hrow1 = hrow0 + RPP;
-  const int lds0 = hrow0 * ROWB + ((lch ^ ((hrow0 >> 1) & 7)) << 4);
-  const int lds1 = hrow1 * ROWB + ((lch ^ ((hrow1 >> 1) & 7)) << 4);
+  const int lds0 = hrow0 * ROWB + ((lch ^ hswz(hrow0)) << 4);
+  const int lds1 = hrow1 * ROWB + ((lch ^ hswz(hrow1)) << 4);
   auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
   auto tile_y0img = [&](int k, int& img0, int& y0) {
     const int tileP = tile_p(k);
@@ -2605,7 +2618,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
   const int nimg = a.M / HW, nTP = Cf::ROWS ? a.M / 128 : (nimg + NSEG - 1) / NSEG;
   const int nTC = a.Cout / CONV_BM, S = a.ksplit;
-  const int NI = nTP * nTC * S;
+  // (folded 1x1 shortcut: slices S .. ST-1 run the shortcut's K over its own input, nchx 64-channel chunks)
+  const int S2 = a.sc_split, ST = S + S2, nchx = (a.sc_C1 + a.sc_C2) / 64;
+  const int NI = nTP * nTC * ST;
   const int G = gridDim.x, b = blockIdx.x;
   // XCD-aware: the dispatcher deals block ids round-robin over the 8 XCDs; XCD x takes the
   // contiguous logical range, in which items sharing a (cout tile, slice) -- its weights -- are adjacent
@@ -2617,10 +2632,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     const int L = bl + k * G;
     tp = L % nTP;
     const int r = L / nTP;
-    z = r % S;
-    tc = r / S;
+    z = r % ST;
+    tc = r / ST;
   };
-  auto chunk_lo = [&](int z) { return (nch * z) / S; };
+  // chunk range [lo, hi) of slice z: the 3x3 conv's Cin / 64 chunks over slices 0 .. S-1, the shortcut's over S ..
+  auto chunk_lo = [&](int z) { return z < S ? (nch * z) / S : (nchx * (z - S)) / S2; };
+  auto chunk_hi = [&](int z) { return z < S ? (nch * (z + 1)) / S : (nchx * (z + 1 - S)) / S2; };
   auto block_sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -2653,12 +2670,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     };
     f32x16 acc[4];
     u32x4 ra[P5_RING];
+    // the folded shortcut's A fragments: voffset = this lane's 16 B, soffset = the wave's 32-cout block + chunk + k-step
+    const __amdgpu_buffer_rsrc_t wrx = __builtin_amdgcn_make_buffer_rsrc((void*)a.sc_wfrag, (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t ablkx = (uint32_t)(nchx * 4) * 1024;
+    auto load_ax = [&](int tc, int cc, int st, u32x4& dst) __attribute__((always_inline)) {
+      dst = __builtin_amdgcn_raw_buffer_load_b128(wrx, (uint32_t)lane * 16,
+                                                  (uint32_t)(tc * 4 + wid) * ablkx + (uint32_t)(cc * 4 + st) * 1024, 0);
+    };
+    bool ring = false;  // ra[0 .. P5_RING-2] hold the next 3x3 item's first k-steps
     {
       int tp, tc, z;
       item_of(0, tp, tc, z);
-      const uint32_t ab0 = abase(tc, chunk_lo(z));
+      if (z < S) {
+        const uint32_t ab0 = abase(tc, chunk_lo(z));
 #pragma unroll
-      for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
+        for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
+        ring = true;
+      }
     }
     block_sync();  // B0: stage 0 staged
     TL(1);
@@ -2666,7 +2694,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     for (int k = 0; k < nit; ++k) {
       int tp, tc, z;
       item_of(k, tp, tc, z);
-      const int c0 = chunk_lo(z), c1 = chunk_lo(z + 1);
+      const int c0 = chunk_lo(z), c1 = chunk_hi(z);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2678,11 +2706,55 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[j][r] = 0.0f;
 #endif
+      if (z >= S) {
+        // ---- a folded-shortcut slice: the centre tap of the raw input chunks the halo waves stage, 4 k-steps
+        // a chunk; chunk cc + 1's A fragments load during chunk cc (ra[0..3] / ra[4..7] by chunk parity)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) load_ax(tc, c0, st, ra[st]);
+        auto chunk1 = [&](auto pc, int cc) __attribute__((always_inline)) {
+          constexpr int P = decltype(pc)::value;
+          if (cc + 1 < c1) {
+#pragma unroll
+            for (int st = 0; st < 4; ++st) load_ax(tc, cc + 1, st, ra[4 * (1 - P) + st]);
+          }
+          int tx[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int h = hb[j] + W2 + 1;
+            tx[j] = (q & 1) * HALO + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+          }
+#pragma unroll
+          for (int st = 0; st < 4; ++st) {
+            bf16x8 fx[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) fx[j] = *(const bf16x8*)(smem + (tx[j] ^ (st << 5)));
+            const bf16x8 af = __builtin_bit_cast(bf16x8, ra[4 * P + st]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fx[j], acc[j], 0, 0, 0);
+          }
+          block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
+          ++q;
+        };
+        for (int cc = c0; cc < c1; cc += 2) {
+          chunk1(std::integral_constant<int, 0>{}, cc);
+          if (cc + 1 < c1) chunk1(std::integral_constant<int, 1>{}, cc + 1);
+        }
+        ring = false;
+      } else {
+      if (!ring) {  // (after a shortcut slice) the ring's first k-steps
+        const uint32_t ab0 = abase(tc, c0);
+#pragma unroll
+        for (int s0 = 0; s0 < P5_RING - 1; ++s0) load_a(ab0, s0, ra[s0]);
+      }
       uint32_t nitem = abase(tc, c1 - 1);  // the next item's first chunk (A prefetch across the item boundary)
+      ring = false;
       if (k + 1 < nit) {
         int tp2, tc2, z2;
         item_of(k + 1, tp2, tc2, z2);
-        nitem = abase(tc2, chunk_lo(z2));
+        if (z2 < S) {
+          nitem = abase(tc2, chunk_lo(z2));
+          ring = true;
+        }
       }
       for (int cc = c0; cc < c1; ++cc, ++q) {
         const char* hcur = smem + (q & 1) * HALO;
@@ -2747,6 +2819,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
         if (q == 0) TL(7);
       }
+      }  // (3x3 slice)
 #if defined(ITSD_DIAG) && defined(P5_CHAINS2)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] += acc2[j];
@@ -2754,14 +2827,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       TL(2);
       // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines
       const int tile = tc * nTP + tp;
-      if (S > 1) {
+      if (ST > 1) {
         // Guideline 16's R1 hand-off, per wave: the partial is stored write-through (sc1), the wave
         // drains its stores, then adds to its (tile, wave) counter; the wave whose add returns S-1 reads
         // every partial with sc1 loads (past its own L1) -- no release / acquire fence, whose L2
         // write-back / L1 invalidate cost ~2-7 us per episode (MI355X_MICROARCH.md, visibility table)
         const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
             a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
-        const uint32_t wbase = (uint32_t)(((size_t)tile * S * 4 + wid) * 4096 * 4) + lane * 16;
+        const uint32_t wbase = (uint32_t)(((size_t)tile * ST * 4 + wid) * 4096 * 4) + lane * 16;
         const uint32_t zstride = 4 * 4096 * 4;  // bytes between the slices of one (tile, wave)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -2775,11 +2848,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         int old = 0;
         if (lane == 0) old = __hip_atomic_fetch_add(a.tickets + tile * 4 + wid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         old = __builtin_amdgcn_readfirstlane(old);
-        if (old != S - 1) continue;  // another slice finishes this tile
+        if (old != ST - 1) continue;  // another slice finishes this tile
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the add)
         if (lane == 0) __hip_atomic_store(a.tickets + tile * 4 + wid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every slice's partial (this one's included), summed in slice order
-        for (int sl = 0; sl < S; ++sl) {
+        for (int sl = 0; sl < ST; ++sl) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -2917,19 +2990,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     TL(7);
   }
 #endif
-  const int nrec1 = (int)std::min<long long>((long long)a.M * a.C1 * 2, 0x7fffffffLL);
-  const int nrec2 = (int)std::min<long long>((long long)a.M * a.C2 * 2, 0x7fffffffLL);
   struct Src {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t rowb, so;
   };
-  auto src_of = [&](int cc) __attribute__((always_inline)) {
+  // chunk cc of the 3x3 conv's input (src1 ++ src2) or, raw, of the folded shortcut's (sc_src1 ++ sc_src2); every
+  // operand of the selects a prvalue (a conditional over the argument block's lvalues selects between field
+  // ADDRESSES: the block could no longer live in registers and went to scratch)
+  auto src_of = [&](int cc, bool raw) __attribute__((always_inline)) {
     const int ci0 = cc * 64;
-    const bool s1 = ci0 < a.C1;
+    const int C1 = raw ? static_cast<int>(a.sc_C1) : static_cast<int>(a.C1);
+    const int C2 = raw ? static_cast<int>(a.sc_C2) : static_cast<int>(a.C2);
+    const bool s1 = ci0 < C1;
+    const void* p = raw ? (s1 ? static_cast<const void*>(a.sc_src1) : static_cast<const void*>(a.sc_src2))
+                        : (s1 ? static_cast<const void*>(a.src1) : static_cast<const void*>(a.src2));
+    const int nrec = (int)std::min<long long>((long long)a.M * (s1 ? C1 : C2) * 2, 0x7fffffffLL);
     Src c;
-    c.rs = __builtin_amdgcn_make_buffer_rsrc(s1 ? (void*)a.src1 : (void*)a.src2, (short)0, s1 ? nrec1 : nrec2, 0x00020000);
-    c.rowb = (uint32_t)(s1 ? a.C1 : a.C2) * 2;
-    c.so = (uint32_t)(s1 ? ci0 : ci0 - a.C1) * 2;
+    c.rs = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nrec, 0x00020000);
+    c.rowb = (uint32_t)(s1 ? C1 : C2) * 2;
+    c.so = (uint32_t)(s1 ? ci0 : ci0 - C1) * 2;
     return c;
   };
   // the stage sequence of this block: (item k, chunk cc); E = the next stage to emit (its data in
@@ -2937,6 +3016,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   u32x4 h[ITEMS];
   f32x4 c[4], cn[4];
   uint32_t zm = 0, zmn = 0;      // bit j: item j of the emitted / loaded stage is real input (else zero)
+  bool rawE = false, rawL = false;  // the emitted / loaded stage is a folded-shortcut chunk (copied, no GroupNorm+SiLU)
   int kL = 0, ccL = 0, c1L = 0;  // the stage being loaded and its item's chunk end
   int pix0 = 0;                  // global pixel of this thread's item 0 of the loaded stage (r = lt >> 3)
   const float* cbase = a.gn_coef;
@@ -3015,7 +3095,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     int tp, tc, z;
     item_of(k, tp, tc, z);
     ccL = chunk_lo(z);
-    c1L = chunk_lo(z + 1);
+    c1L = chunk_hi(z);
+    rawL = z >= S;
     const int img = Cf::ROWS ? (tp * 128) / HW : tp * NSEG + sg;
     const int y0 = Cf::ROWS ? ((tp * 128) % HW) / W : 0;  // the tile's first image row
     const int imgc = img < nimg ? img : nimg - 1;
@@ -3031,6 +3112,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   // stage L's GroupNorm+SiLU coefficients of this lane's 8 channels (gn_fold: gamma / beta, turned
   // into a, b by prescale from the wave's group statistics)
   auto load_stage = [&]() __attribute__((always_inline)) {
+    if (rawL) return;
     if (a.gn_fold) {
       const int c0 = ccL * 64 + 8 * lch;
       cn[0] = *(const f32x4*)(a.gn_gamma + c0);
@@ -3044,6 +3126,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     }
   };
   auto prescale = [&]() __attribute__((always_inline)) {
+    rawE = rawL;
+    if (rawL) {
+      zm = zmn;
+      return;
+    }
     if (a.gn_fold) {  // a = rstd gamma, b = beta - mean a (gn_coef_kernel's formula), per channel's group
       const int c0 = ccL * 64 + 8 * lch;
       const float rg = 32.0f / (float)Cin;  // group = floor((c + 0.5) / gsz) (exact: c < 2^11, gsz <= 64)
@@ -3069,7 +3156,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     if (++ccL == c1L) {
       if (++kL < nit) {
         open_item(kL);
-        if (a.gn_fold) group_stats(kL);
+        if (a.gn_fold && !rawL) group_stats(kL);
       } else {
         more = false;
       }
@@ -3079,15 +3166,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   auto emit = [&](char* hbuf) __attribute__((always_inline)) {
     const bool live = more;
     if (live) load_stage();
-    const Src nx = src_of(live ? ccL : 0);
+    const Src nx = src_of(live ? ccL : 0, live && rawL);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       uint32_t yw[4];
       const uint32_t zj = (uint32_t)__builtin_amdgcn_sbfe((int)zm, j, 1);  // 0 (padding) or ~0
+      if (rawE) {
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-        gn_silu_x4(h[j][2 * hf], h[j][2 * hf + 1], c[hf][0], c[hf][1], c[hf][2], c[hf][3], c[2 + hf][0],
-                   c[2 + hf][1], c[2 + hf][2], c[2 + hf][3], zj, yw[2 * hf], yw[2 * hf + 1]);
+        for (int e = 0; e < 4; ++e) yw[e] = h[j][e] & zj;
+      } else {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+          gn_silu_x4(h[j][2 * hf], h[j][2 * hf + 1], c[hf][0], c[hf][1], c[hf][2], c[hf][3], c[2 + hf][0],
+                     c[2 + hf][1], c[2 + hf][2], c[2 + hf][3], zj, yw[2 * hf], yw[2 * hf + 1]);
+      }
       *(u32x4*)(hbuf + lds[j]) = u32x4{yw[0], yw[1], yw[2], yw[3]};
       __builtin_amdgcn_sched_barrier(0);
       const uint32_t pix = live && ((zmn >> j) & 1) ? (uint32_t)(pix0 + RPP * j) : 0u;
@@ -3132,7 +3224,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   open_item(0);
   load_stage();
   {
-    const Src s0 = src_of(ccL);
+    const Src s0 = src_of(ccL, rawL);
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
       h[j] = __builtin_amdgcn_raw_buffer_load_b128(
@@ -3146,7 +3238,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     if (x == 0 || x == W2 - 1 || (!Cf::ROWS && (y == 0 || y == TH + 1)))
       *(u32x4*)(smem + buf * HALO + row * ROWB + ((u & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
   }
-  if (a.gn_fold) group_stats(0);
+  if (a.gn_fold && !rawL) group_stats(0);
   TL(1);
   prescale();
   advance();
@@ -3159,7 +3251,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   for (int k = 0; k < nit; ++k) {
     int tp, tc, z;
     item_of(k, tp, tc, z);
-    const int c0 = chunk_lo(z), c1 = chunk_lo(z + 1);
+    const int c0 = chunk_lo(z), c1 = chunk_hi(z);
     for (int cc = c0; cc < c1; ++cc, ++q) {
       if (cc == c0) stage_addv(k);
       // the item's residual, during its last stage; landed before that stage's barrier (only the next
@@ -3499,13 +3591,56 @@ bool conv_p5_selected(const ConvArgs& a) {
   return a.Wout == 4 || a.Wout == 64 || g_p5 == 2 || (g_p5 == 1 && p4_tiles < 192);
 }
 
+// The ResBlock's 1x1 shortcut as extra K slices of its block2 conv on p5 (ConvArgs sc_*): the (S, S2) 3x3 /
+// shortcut slice counts minimising ceil(items / CUs) x the slower slice + the combine, in chunk-times (a 3x3
+// chunk = 1; a shortcut chunk ~0.4: 4 of its 36 k-steps, the same staging; prologue / epilogue 1.5); folded
+// where that beats the unfolded plan plus the standalone 1x1 launch it replaces (~3 chunk-times: a 10-17 us
+// launch at these sizes), or always with g_p5_sc = 2. Returns S2 (0: not folded) and the S to run with.
+static int p5_plan(const ConvArgs& a, int* S_out) {
+  const int HW = a.Hout * a.Wout, nimg = a.M / HW;
+  const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
+  const int tiles = ptiles * (a.Cout / CONV_BM), nch = (a.C1 + a.C2) / 64, nchx = (a.sc_C1 + a.sc_C2) / 64;
+  const bool ws = a.splitk_ws && a.tickets;
+  const int S0 = ws ? p5_split(a, tiles, nch) : 1;
+  *S_out = S0;
+  if (!ws || !g_p5_sc || !a.sc_wfrag || nchx == 0 || a.sc_C1 % 64 || a.sc_C2 % 64 || (long long)tiles * 4 > kTicketCap)
+    return 0;
+  auto cost = [&](int s, int s2) {
+    const double waves = std::ceil((double)tiles * (s + s2) / g_num_cus);
+    const double c3 = std::ceil((double)nch / s) + 1.5, c1 = s2 ? 0.4 * std::ceil((double)nchx / s2) + 1.5 : 0.0;
+    return waves * std::max(c3, c1) + (s + s2 > 1 ? 0.3 * (s + s2) : 0.0);
+  };
+  double best = 1e30;
+  int bs = 0, bs2 = 0;
+  const int slo = g_p5_split > 0 ? S0 : 1, shi = g_p5_split > 0 ? S0 : std::min(nch, 16);
+  for (int s = slo; s <= shi; ++s)
+    for (int s2 = 1; s2 <= std::min(nchx, 16); ++s2) {
+      if ((long long)tiles * (s + s2) * 4 * 4096 > a.splitk_cap) break;
+      const double c = cost(s, s2);
+      if (c < best - 1e-9) { best = c; bs = s; bs2 = s2; }
+    }
+  if (!bs2 || (g_p5_sc != 2 && best >= cost(S0, 0) + 3.0)) return 0;
+  *S_out = bs;
+  return bs2;
+}
+
+// launch_conv's shortcut fold for a p5 conv carrying sc_* candidates: folded?
+bool conv_p5_sc_fold(const ConvArgs& a) {
+  int S;
+  return conv_p5_selected(a) && p5_plan(a, &S) > 0;
+}
+
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
   const int HW = a.Hout * a.Wout, nimg = a.M / HW;
   const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
-  const int tiles = ptiles * (a.Cout / CONV_BM), nch = (a.C1 + a.C2) / 64;
-  a.ksplit = (a.splitk_ws && a.tickets) ? p5_split(a, tiles, nch) : 1;
-  const int items = tiles * a.ksplit;
+  const int tiles = ptiles * (a.Cout / CONV_BM);
+  int S = 1;
+  const int S2 = p5_plan(a, &S);
+  if (a.sc_C1 + a.sc_C2 && !S2) return hipErrorInvalidValue;  // (the caller folds only what p5_plan accepts)
+  a.ksplit = S;
+  a.sc_split = S2;
+  const int items = tiles * (S + S2);
   const dim3 g(std::min(items, g_num_cus));
   if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p5_kernel<64>, g, dim3(512), 0, s, a);
   else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);

@@ -98,6 +98,10 @@ def test_conv_tile_options():
         rt.set_option("p4_c96", v)
     with pytest.raises(rt.ItsdError):
         rt.set_option("p4_c96", 3)
+    for v in (0, 2, 1):  # 1x1 shortcuts as K slices of their block2 p5 conv: off / always / auto (shipped)
+        rt.set_option("p5_sc", v)
+    with pytest.raises(rt.ItsdError):
+        rt.set_option("p5_sc", 3)
     rt.set_option("spin_bound", 0)  # diagnostic (fail-loud hand-off test), any bound >= 0
     rt.set_option("spin_bound", 1 << 22)
     with pytest.raises(rt.ItsdError):
