@@ -1444,6 +1444,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #ifndef ITSD_P4_M16
 #define ITSD_P4_M16 2
 #endif
+#ifndef ITSD_P4_ZR8
+#define ITSD_P4_ZR8 1  // COMPACT 16x16x32 forms: 8 zero rows (a padding lane keeps its bank slot; 0: one, A/B builds)
+#endif
 #ifndef ITSD_P4_HSWZ
 #define ITSD_P4_HSWZ 1  // the 16x16x32 forms' halo swizzle h & 6 (0: (h >> 1) & 7, as the 32x32x16 forms; A/B builds)
 #endif
@@ -1480,9 +1483,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // M16: the MFMA waves on v_mfma_f32_16x16x32_bf16 (the LDS residual / output tile forms; the sub-pixel and
   // register-epilogue forms stay on 32x32x16). ITSD_P4_M16: 0 none, 1 the 32x32 level, 2 every RES form
   constexpr bool M16 = ITSD_P4_M16 >= 1 && RES && !SUB && (AB & 1) == 0 && (W == 32 || ITSD_P4_M16 >= 2);
-  // (COMPACT + M16: a second zero row 64 rows past the first, so that a lane pointed at the zero row reads zeros at
-  // the +64-row immediate offset of its pixel blocks 4..7 too)
-  constexpr int ZROWS = COMPACT ? (M16 ? 65 : 1) : 0;
+  // (COMPACT + M16: 8 zero rows, a lane whose tap falls outside its image reads the one with its own row's residue
+  // mod 8 -- its own bank slot under hswz, so the zero reads do not collide with the group's real rows -- and 8 more
+  // 64 rows past them, read at the +64-row immediate offset of pixel blocks 4..7)
+  constexpr int ZROWS = COMPACT ? (M16 ? (ITSD_P4_ZR8 ? 72 : 65) : 1) : 0;
   // halo row h's 16-B units are stored XOR-permuted by hswz(h). ds_read_b128 serves a wave in four 16-lane groups
   // ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, +32: MI355X_MICROARCH.md, LDS) over 16 slots of 16 B (row parity x
   // unit). The 32x32x16 B reads (lane = 32 rows x 2 halves) are conflict-free for any tap offset with
@@ -1721,7 +1725,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
                 // block t: x = column, y = row in its image (y range checked at 8x8 only: 16x16 rows are wave-uniform)
                 const int x = (p0 & (W - 1)) + kx - 1, y = (((p0 / W) + t * (16 / W)) & (W - 1)) + ky - 1;
                 const bool ok = (unsigned)x < (unsigned)W && (W == 16 || (unsigned)y < (unsigned)W);
-                h = ok ? p0 + 16 * t + (ky - 1) * W + (kx - 1) : ZROW;
+                const int hw = p0 + 16 * t + (ky - 1) * W + (kx - 1);
+                h = ok ? hw : ZROW + (ITSD_P4_ZR8 && W == 8 ? (hw & 7) : 0);  // (16x16: one zero row; a spill otherwise)
               } else {
                 h = p0 + t * W2 + ky * W2 + kx;  // block 2t
               }
@@ -2499,8 +2504,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   }
   if constexpr (COMPACT) {  // the zero row of both halo buffers (no stage writes it; read after B0)
     if (tt < 16) *(u32x4*)(smem + (tt >> 3) * HALO + ZROW * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
-    if (M16 && tt >= 16 && tt < 32)
+    if (M16 && ITSD_P4_ZR8) {  // rows ZROW + 0..7 and + 64..71 of both buffers: one 16-B unit a thread
+      const int r = (tt >> 3) & 15;
+      *(u32x4*)(smem + (tt >> 7) * HALO + (ZROW + (r & 7) + (r >> 3) * 64) * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
+    } else if (M16 && tt >= 16 && tt < 32) {
       *(u32x4*)(smem + ((tt >> 3) & 1) * HALO + (ZROW + 64) * ROWB + ((tt & 7) << 4)) = u32x4{0u, 0u, 0u, 0u};
+    }
   }
   emit(smem);
 #ifdef ITSD_STAMPS
