@@ -1447,6 +1447,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #ifndef ITSD_P4_ZR8
 #define ITSD_P4_ZR8 1  // COMPACT 16x16x32 forms: 8 zero rows (a padding lane keeps its bank slot; 0: one, A/B builds)
 #endif
+#ifndef ITSD_P5_SWZ
+#define ITSD_P5_SWZ 1  // conv3x3_gn_p5_kernel's per-level halo swizzle at W <= 16 (0: (h >> 1) & 7; A/B builds)
+#endif
 #ifndef ITSD_P4_HSWZ
 #define ITSD_P4_HSWZ 1  // the 16x16x32 forms' halo swizzle h & 6 (0: (h >> 1) & 7, as the 32x32x16 forms; A/B builds)
 #endif
@@ -2605,6 +2608,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   constexpr int HW = Cf::HW, NSEG = Cf::NSEG, W2 = Cf::W2, HS = Cf::HS, TPS = Cf::TPS, RPP = Cf::RPP;
   constexpr int ITEMS = Cf::ITEMS, HALO = Cf::HALO, TH = Cf::TH, HY0 = Cf::HY0, NHY = Cf::NHY;
   constexpr int SPX = TH * W;  // pixels of one segment
+  // halo row (hy, hx) -> its 16-B units XOR-permuted by swz: ds_read_b128 serves the MFMA waves' B reads in 16-lane
+  // groups ({0-3, 12-15, 20-27}, ...) of 16 pixels, which at W <= 16 span 2-4 image rows of a segment, non-contiguous
+  // halo rows; (h >> 1) & 7 left 37 % (W = 4 / 8) and 12 % (W = 16) of those lanes on a taken bank slot -- the p5<4>
+  // launch's 4.8e6 conflict cycles (profiles/r05/pmc_dispatch_table_r05ae.txt). A slot is (hx & 1, swz) (W2 even);
+  // these keep every group of every tap on 16 distinct slots (exhaustive check: tools/halo_swizzle.py --p5)
+  constexpr int SC1 = 1, SC2 = W <= 8 ? 2 : 1;
+  auto swz = [](int hy, int hx, int h) { return W <= 16 && ITSD_P5_SWZ ? (SC1 * hy + SC2 * hx) & 7 : (h >> 1) & 7; };
   static_assert(NSEG * SPX == 128 && ITEMS * RPP == NHY * W && ITEMS <= 31 && 36 % P5_RING == 0, "p5 geometry");
   constexpr int SEGW = 64 / TPS > 0 ? 64 / TPS : 1;  // image segments one halo wave covers (W = 4: 2)
   // + the residual tiles of two items [item parity][128 px][128 couts] bf16 (LDS-DMA'd by the halo waves
@@ -2657,11 +2667,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     // ================================================================ MFMA waves
     const int rl = lane & 31, hh = lane >> 5;
     int hb[4];  // halo row of this lane's pixel (tap 0, 0) in each 32-pixel block
+    int hq[4];  // its swz coordinates SC1 y + SC2 x (W <= 16)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pl = j * 32 + rl, seg = pl / SPX, rem = pl - seg * SPX, y = rem / W;
       hb[j] = seg * HS + y * W2 + (rem - y * W);
+      hq[j] = SC1 * y + SC2 * (rem - y * W);
     }
+    // B unit of pixel block j at tap (ky, kx): halo row h = hb[j] + ky W2 + kx, hy = y + ky, hx = x + kx
+    auto bunit = [&](int j, int h, int ky, int kx) {
+      return W <= 16 && ITSD_P5_SWZ ? (hq[j] + SC1 * ky + SC2 * kx) & 7 : (h >> 1) & 7;
+    };
     const uint32_t ablk = (uint32_t)(9 * kpt) * 1024;  // one 32-cout block of fragments
     // A fragments by buffer loads (conv3x3_gn_p4_kernel's scheme): voffset = this lane's 16 B of the wave's
     // 32-cout block, soffset = the tile's fragment block + chunk + k-step (uniform scalar arithmetic)
@@ -2730,7 +2746,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int h = hb[j] + W2 + 1;
-            tx[j] = (q & 1) * HALO + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+            tx[j] = (q & 1) * HALO + h * ROWB + ((hh ^ bunit(j, h, 1, 1)) << 4);
           }
 #pragma unroll
           for (int st = 0; st < 4; ++st) {
@@ -2778,7 +2794,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             for (int j = 0; j < 4; ++j) {
               int h = hb[j] + ky * W2 + kx;
               asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
-              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ bunit(j, h, ky, kx)) << 4);
             }
           }
 #if defined(ITSD_DIAG) && defined(P5_AB)
@@ -2989,7 +3005,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   for (int j = 0; j < ITEMS; ++j) {
     const int r = (lt >> 3) + RPP * j, hy = HY0 + r / W, x = r - (r / W) * W;
     const int hrow = sg * HS + hy * W2 + (x + 1);
-    lds[j] = hrow * ROWB + ((lch ^ ((hrow >> 1) & 7)) << 4);
+    lds[j] = hrow * ROWB + ((lch ^ swz(hy, x + 1, hrow)) << 4);
   }
 #ifdef ITSD_STAMPS
   {  // timeline: the kernel arguments are in SGPRs (a first dependent use)
