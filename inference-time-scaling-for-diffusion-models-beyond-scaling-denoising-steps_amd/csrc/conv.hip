@@ -1450,6 +1450,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #ifndef ITSD_P5_SWZ
 #define ITSD_P5_SWZ 1  // conv3x3_gn_p5_kernel's per-level halo swizzle at W <= 16 (0: (h >> 1) & 7; A/B builds)
 #endif
+#ifndef ITSD_P4_SUBSWZ
+#define ITSD_P4_SUBSWZ 1  // p4's non-compact 8x8 / 16x16 halo (sub-pixel forms) swizzled by halo coordinates (0: (h >> 1) & 7)
+#endif
 #ifndef ITSD_P4_HSWZ
 #define ITSD_P4_HSWZ 1  // the 16x16x32 forms' halo swizzle h & 6 (0: (h >> 1) & 7, as the 32x32x16 forms; A/B builds)
 #endif
@@ -1498,6 +1501,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   // SQ_LDS_BANK_CONFLICT, profiles/r05/p4_lds_conflicts_r05ab.txt), and are conflict-free at every offset with
   // h & 6 (exhaustive check over offsets, groups and both half-steps: tools/halo_swizzle.py)
   auto hswz = [](int h) { return M16 && ITSD_P4_HSWZ ? (h & 6) : ((h >> 1) & 7); };
+  // The non-compact halo at 8x8 / 16x16 (the sub-pixel forms' input grids): a 32-pixel block spans image rows of
+  // W + 2-row pitch, so (h >> 1) & 7 left 37 % / 12 % of the 32x32x16 B reads' lanes on a taken bank slot (9.4e6
+  // conflict cycles a <8, 128> / <16, 128> launch at N = 256); halo coordinates instead: unit ^ (hy + SC2 hx) & 7
+  // (as conv3x3_gn_p5_kernel's halo; tools/halo_swizzle.py --p5 geometry)
+  constexpr bool CSWZ = ITSD_P4_SUBSWZ && !COMPACT && !M16 && W <= 16;
+  constexpr int SC1 = 1, SC2 = W <= 8 ? 2 : 1;
   // C96 (AB bit 512, 8x8 only): 96-cout tiles -- Cout = 384 gives 4 cout tiles, so N = 256's 64 pixel tiles make
   // 256 tiles for the 256 CUs instead of 192 with 128 couts (a quarter of the chip idle). Each MFMA wave holds 48
   // couts (3 16x16 blocks); the LDS output tile keeps its 64-cout halves (48 used: units 0..5 of 8)
@@ -1729,7 +1738,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
                 const int x = (p0 & (W - 1)) + kx - 1, y = (((p0 / W) + t * (16 / W)) & (W - 1)) + ky - 1;
                 const bool ok = (unsigned)x < (unsigned)W && (W == 16 || (unsigned)y < (unsigned)W);
                 const int hw = p0 + 16 * t + (ky - 1) * W + (kx - 1);
-                h = ok ? hw : ZROW + (ITSD_P4_ZR8 && W == 8 ? (hw & 7) : 0);  // (16x16: one zero row; a spill otherwise)
+                h = ok ? hw : ZROW + (ITSD_P4_ZR8 && W == 8 ? (hw & 7) : 0);  // (16x16: one zero row; 8 rows by residue spilled)
               } else {
                 h = p0 + t * W2 + ky * W2 + kx;  // block 2t
               }
@@ -1835,11 +1844,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
     // +127 (four B fragments): 8 MFMAs per k-step on 128 accumulator registers (AGPRs)
     const int wm = wid & 1, wn = wid >> 1, rl = lane & 31, hh = lane >> 5;
     int hb[4];  // halo row of this lane's pixel at tap (0, 0) (COMPACT: the tile pixel itself)
+    int hq[4];  // (CSWZ) its coordinate swizzle base SC1 oy + SC2 ox
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pl = wn * 128 + j * 32 + rl;
       const int seg = pl / (THs * W), rem = pl - seg * THs * W, oy = rem / W;
       hb[j] = COMPACT ? pl : seg * HS + oy * W2 + (rem - oy * W);
+      hq[j] = SC1 * oy + SC2 * (rem - oy * W);
     }
     const uint32_t ablk = (uint32_t)(NTAP * kpt) * 1024;  // one 32-cout block of fragments
     // A fragments by buffer loads: resource = the whole wfrag array, voffset = this lane's 16 B of the wave's
@@ -1966,7 +1977,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
                 h = hb[j] + ky * W2 + kx;
                 asm volatile("" : "+v"(h));
               }
-              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ ((h >> 1) & 7)) << 4);
+              const int sw = CSWZ ? (hq[j] + SC1 * ky + SC2 * kx) & 7 : (h >> 1) & 7;
+              tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ sw) << 4);
             }
           }
 #pragma unroll
@@ -2203,7 +2215,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p4_kernel(ConvArgs a) {
   const int hrow0 = (COMPACT ? sg * HWs : sg * HS) + (lt >> 3), hrow1 = hrow0 + RPP;
   const int lds0 = hrow0 * ROWB + ((lch ^ hswz(hrow0)) << 4);
   const int lds1 = hrow1 * ROWB + ((lch ^ hswz(hrow1)) << 4);
-  auto item_lds = [&](int j) { return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB); };
+  auto item_lds = [&](int j) {
+    if constexpr (CSWZ) {  // (halo coordinates of the item's row; the scratch rows past HS go to dump)
+      const int r = (lt >> 3) + RPP * j, hy = r / W2, hx = r - hy * W2;
+      return (sg * HS + r) * ROWB + ((lch ^ ((SC1 * hy + SC2 * hx) & 7)) << 4);
+    }
+    return ((j & 1) ? lds1 : lds0) + (j >> 1) * (2 * RPP * ROWB);
+  };
   auto tile_y0img = [&](int k, int& img0, int& y0) {
     const int tileP = tile_p(k);
     img0 = tileP / (H * W);

@@ -1799,7 +1799,7 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 // bf16 tail on MFMA with the tail GroupNorm+SiLU fused (Model.py:252-256 / 282, then the
 // sampler step as tail2_kernel). Block = 128 output pixels (128/W rows) of one image; the
 // raw input halo ((128/W + 2) x (W + 2) pixels x C) is staged once in LDS with
-// y = silu(x*a + b) applied (padding stays 0), at a padded pixel stride (conflict-free
+// y = silu(x*a + b) applied (padding stays 0), at a padded pixel stride (tail_pst: conflict-free
 // 16-B fragment reads); the staging issues 8 loads per thread before transforming any
 // (HBM latency once per batch, not per chunk). Each wave owns 2 x 16 pixels:
 // eps[pixel][co] = sum_k patch[pixel][k] W[co][k] on v_mfma_f32_16x16x32_bf16
@@ -1807,13 +1807,22 @@ __global__ __launch_bounds__(256) void tail2_kernel(TailArgs a) {
 // TM_PX output pixels per block: 128 (64 -- a smaller halo, 3 blocks a CU -- measured +0.3 %, removed in round 5);
 // NTH threads: 512 (round 5: 8 waves, one 16-pixel group each -- twice the waves a CU for the halo transform's
 // latency: 71.1 -> 65.5 us a launch at N = 256 against 256 threads, profiles/r05/tail_512_vs_256_r05x.txt)
+// Halo pixel stride (bytes): 2C + 32 = (C / 8 + 2) x 16 B, == 2 (mod 4) 16-B units for C % 32 == 0. An A-fragment
+// ds_read_b128 group ({0-3, 12-15, 20-27}, ...: 8 pixels of one k-group + 8 of the next) then lands on 16 distinct
+// 16-B slots, the two k-groups on opposite slot parities (2C + 16, one unit odd, put pixel m + 1 of one k-group on
+// pixel m's slot of the other: 6.8e6 bank-conflict cycles a launch at N = 256, profiles/r05/pmc_dispatch_table_r05ae.txt)
+#ifndef ITSD_TAIL_PAD32
+#define ITSD_TAIL_PAD32 1  // (0: 2C + 16, A/B builds)
+#endif
+__host__ __device__ constexpr int tail_pst(int C) { return 2 * C + (ITSD_TAIL_PAD32 ? 32 : 16); }
+
 template <int TM_PX, int NTH>
 __global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
   constexpr int NW = NTH / 64, GPW = TM_PX / 16 / NW;  // waves; 16-pixel MFMA groups a wave
   static_assert(GPW >= 1 && GPW * 16 * NW == TM_PX, "tail geometry");
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   const int C = a.C, W = a.W, H = a.H, HW = H * W;
-  const int rpb = TM_PX / W, bpi = H / rpb, PST = 2 * C + 16, NKS = 9 * C / 32;
+  const int rpb = TM_PX / W, bpi = H / rpb, PST = tail_pst(C), NKS = 9 * C / 32;
   const int img = blockIdx.x / bpi, y0 = (blockIdx.x % bpi) * rpb;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   bf16x8* wl = (bf16x8*)tsm;                                   // [NKS][4][3]
@@ -1967,7 +1976,7 @@ __global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
 }
 
 static size_t tail_mfma_smem_px(int px, int H, int W, int C) {
-  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(px / W + 2) * (W + 2) * (2 * C + 16) + 2 * px * 3 * 4 +
+  return (size_t)(9 * C / 32) * 12 * 16 + (size_t)(px / W + 2) * (W + 2) * tail_pst(C) + 2 * px * 3 * 4 +
          (size_t)C * 2 * 4;
 }
 static bool tail_mfma_ok_px(int px, int H, int W, int C) {
