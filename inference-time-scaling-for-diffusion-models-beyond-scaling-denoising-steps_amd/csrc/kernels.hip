@@ -1129,7 +1129,8 @@ hipError_t launch_attn_block(const AttnBlockArgs& a, int C, hipStream_t s) {
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
-// S = 64: one image a block (LDS: C <= 384); S = 16 (the 4x4 middle block): 4 images a block, C <= 512
+// S = 64: one image a block (LDS: C <= 384). (The 4x4 middle block's 4-images-a-block form measured slower at N = 32
+// and was removed in round 5: that AttnBlock runs the unfused GroupNorm / q|k|v / attention / proj launches.)
 bool attn_block_ok(int S, int C) {
   return S == 64 && (C == 128 || C == 256 || C == 384);
 }
