@@ -2612,9 +2612,15 @@ template <int W> struct Gp5Cfg {
   static constexpr int TPS = 256 / NSEG, RPP = TPS / 8, ITEMS = NHY * W / RPP;
   static constexpr int HALO = ((NSEG * HS * ROWB) + 1023) & ~1023;  // one halo buffer (bytes)
 };
-constexpr int P5_RING = 9;  // A k-step slots (prefetch distance 8 k-steps = 32 MFMAs); divides 36
+#ifndef ITSD_P5_RING
+#define ITSD_P5_RING 9
+#endif
+#ifndef ITSD_P5_BD
+#define ITSD_P5_BD 3
+#endif
+constexpr int P5_RING = ITSD_P5_RING;  // A k-step slots (prefetch distance 8 k-steps = 32 MFMAs); divides 36
                             // (12 and 18 measured equal at N = 32 and 256)
-constexpr int P5_BD = 3;    // B fragment buffers (reads two k-steps = 8 MFMAs ahead)
+constexpr int P5_BD = ITSD_P5_BD;    // B fragment buffers (reads two k-steps = 8 MFMAs ahead)
 // (round 5: the MFMA waves on v_mfma_f32_16x16x32_bf16 as in p4 -- 2 x 8 f32x4 accumulators, 6-slot k32 A ring, 8-B
 // stores, per-slot butterflies over the 16 pixel lanes -- measured N = 256 equal, N = 32 +2.3 %, N = 64 +0.7 %, C4
 // +0.7 % step time against this form, profiles/r05/step_p5_m16_vs_m32.txt: removed)
