@@ -1829,7 +1829,7 @@ __global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
   bf16x8* wl = (bf16x8*)tsm;                                   // [NKS][4][3]
   char* halo = tsm + NKS * 12 * 16;                            // [(rpb+2)*(W+2)][PST]
   float* red = (float*)(halo + (rpb + 2) * (W + 2) * PST);     // [2 passes][TM_PX][3]
-  float* cfl = red + 2 * TM_PX * 3;                            // [C/8][16] this pass's GN coefficients
+  float* cfl = red + 2 * TM_PX * 3;                            // [4][C/8][4] this pass's GN coefficients
   const int m = lane & 15, kg = lane >> 4;
   int hbase[GPW];
 #pragma unroll
@@ -1884,7 +1884,12 @@ __global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
       }
       if (i0 == 0) {  // the image's GroupNorm coefficients (and, first pass, the weights) into LDS, their
                       // loads behind the batch's: one memory round trip for all of them
-        for (int i = tid; i < cpp * 16; i += NTH) cfl[i] = a.coef[(size_t)im * cpp * 16 + i];
+        // (coef[img][C/8][a0..a7, b0..b7] -> quarter q of chunk ch at (q C/8 + ch) x 16 B: the 16 chunks a 16-lane
+        // read group stages are then 256 contiguous bytes, not 64-B strided -- a 4-way conflict on every read)
+        for (int i = tid; i < cpp * 16; i += NTH) {
+          const int ch = i >> 4, e = i & 15;
+          cfl[((e >> 2) * cpp + ch) * 4 + (e & 3)] = a.coef[(size_t)im * cpp * 16 + i];
+        }
         if (pass == 0)
           for (int i = tid; i < NKS * 12; i += NTH) wl[i] = *(const bf16x8*)(a.wmf + (size_t)i * 8);
         __syncthreads();
@@ -1896,8 +1901,8 @@ __global__ __launch_bounds__(NTH, 2) void tail_mfma_kernel(TailArgs a) {
         int d = dst[u];
         if (d >= 0) {
           const int ch = (d % PST) / 16;
-          const f32x4* cp = (const f32x4*)(cfl + ch * 16);
-          const f32x4 a0 = cp[0], a1 = cp[1], b0 = cp[2], b1 = cp[3];
+          const f32x4* cp = (const f32x4*)cfl + ch;
+          const f32x4 a0 = cp[0], a1 = cp[cpp], b0 = cp[2 * cpp], b1 = cp[3 * cpp];
           // silu(v) = v / (1 + 2^(-v log2 e)): one exp2 and one rcp (the result is rounded to bf16)
           auto fsilu = [](float v) { return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f)); };
 #pragma unroll
