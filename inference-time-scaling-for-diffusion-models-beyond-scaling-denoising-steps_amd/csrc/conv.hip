@@ -1447,6 +1447,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #ifndef ITSD_P4_ZR8
 #define ITSD_P4_ZR8 1  // COMPACT 16x16x32 forms: 8 zero rows (a padding lane keeps its bank slot; 0: one, A/B builds)
 #endif
+#ifndef ITSD_P5_SC_LAUNCH
+#define ITSD_P5_SC_LAUNCH 5.0  // the standalone 1x1 launch a folded shortcut saves, in p5 chunk-times (3: r05aq A/B)
+#endif
 #ifndef ITSD_P5_SWZ
 #define ITSD_P5_SWZ 1  // conv3x3_gn_p5_kernel's per-level halo swizzle at W <= 16 (0: (h >> 1) & 7; A/B builds)
 #endif
@@ -3643,8 +3646,10 @@ bool conv_p5_selected(const ConvArgs& a) {
 // The ResBlock's 1x1 shortcut as extra K slices of its block2 conv on p5 (ConvArgs sc_*): the (S, S2) 3x3 /
 // shortcut slice counts minimising ceil(items / CUs) x the slower slice + the combine, in chunk-times (a 3x3
 // chunk = 1; a shortcut chunk ~0.4: 4 of its 36 k-steps, the same staging; prologue / epilogue 1.5); folded
-// where that beats the unfolded plan plus the standalone 1x1 launch it replaces (~3 chunk-times: a 10-17 us
-// launch at these sizes), or always with g_p5_sc = 2. Returns S2 (0: not folded) and the S to run with.
+// where that beats the unfolded plan plus the standalone 1x1 launch it replaces (ITSD_P5_SC_LAUNCH = 5 chunk-times: a
+// 10-20 us launch with its gap; 3 left the 32x32 shortcuts at N = 32, the 8x8 ones at N = 64 and the 4x4 ones at N = 256
+// unfolded, 0.5-1.1 % slower steps, profiles/r05/p5_sc_launch_cost_r05aq.txt), or always with g_p5_sc = 2. Returns S2
+// (0: not folded) and the S to run with.
 static int p5_plan(const ConvArgs& a, int* S_out) {
   const int HW = a.Hout * a.Wout, nimg = a.M / HW;
   const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
@@ -3668,7 +3673,7 @@ static int p5_plan(const ConvArgs& a, int* S_out) {
       const double c = cost(s, s2);
       if (c < best - 1e-9) { best = c; bs = s; bs2 = s2; }
     }
-  if (!bs2 || (g_p5_sc != 2 && best >= cost(S0, 0) + 3.0)) return 0;
+  if (!bs2 || (g_p5_sc != 2 && best >= cost(S0, 0) + ITSD_P5_SC_LAUNCH)) return 0;
   *S_out = bs;
   return bs2;
 }
