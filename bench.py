@@ -15,8 +15,8 @@ Rank 0 prints ONE JSON line. Extra fields (single-GPU runs):
   roofline      the dominant kernel (fused GroupNorm conv) in steady state with HIP events on
                 the UNet's stream, its PMC HBM traffic (profiles/, this commit), the conv tiles'
                 HBM GB/s, and the attention kernels' MFMA utilisation;
-  sweep         N in {32, 64, 128, 256, 1024} on one GPU (north_star's N set; N = 32 / 64 / 128 are
-                the 8- / 4- / 2-GPU shards of N = 256), same path;
+  sweep         N in {8, 16, 32, 64, 128, 256, 1024} on one GPU (north_star's N set; N = 32 / 64 / 128 are
+                the 8- / 4- / 2-GPU shards of N = 256, N = 8 / 16 those of N = 64 at 8 / 4 GPUs), same path;
   fp32          the reference-precision (parity mode) throughput at the headline N;
   legs          the other BASELINE configs per GPU shard: C3 CFG zero-order round (Arch C,
                 N_local = 32 -> 2N = 64 guided batch), C4 64x64 Arch A (N_local = 16), C5
@@ -501,7 +501,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         # north_star N sweep on the same path (headline N is the main line)
         sweep = {}
-        for n, window in ((32, 1000), (64, 1000), (128, 1000), (256, 1000), (1024, 100)):
+        for n, window in ((8, 1000), (16, 1000), (32, 1000), (64, 1000), (128, 1000), (256, 1000), (1024, 100)):
             if n == n_local:
                 continue
             progress(f"sweep N={n}")

@@ -88,6 +88,7 @@ int fail(int code, const std::string& msg) {
 std::string handoff_msg(int bits) {
   std::string m = "in-kernel hand-off wait exhausted its poll bound (grid not co-resident?):";
   if (bits & 1) m += " attn_block_split_kernel";
+  if (bits & 2) m += " conv3x3_gn_p5_kernel (split-K combine)";
   return m;
 }
 
@@ -915,6 +916,8 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     a.splitk_ws = u->splitk_ws;
     a.splitk_cap = itsd_unet::kSplitkCap;
     a.tickets = u->tickets;
+    a.err = u->d_nan + 1;
+    a.spin_bound = itsd::g_spin_bound;
     if (o.vt >= 0) {
       if (o.vt_from % 128 || (out.H * out.W) % 8) return fail(ITSD_ERR_INVALID, "internal: bad channel-major V split");
       a.vt_out = u->ap(o.vt);
@@ -1367,6 +1370,12 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p5_sc")) {  // ResBlock 1x1 shortcuts as K slices of their block2 p5 conv: 0 off, 1 auto, 2 always
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_sc in [0,2]");
     itsd::g_p5_sc = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p5_dist")) {  // p5's split-K combine shared by every slice (co-resident grids): 0 off (last arriver),
+                                       // 1 on, 2 the same plans as 1 combined by the last arriver (bit-identity checks)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_dist in [0,2]");
+    itsd::g_p5_dist = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p4 / p5_kernel: 0 off, 1 on

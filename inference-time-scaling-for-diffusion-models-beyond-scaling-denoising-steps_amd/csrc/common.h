@@ -31,6 +31,7 @@ extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
 extern int g_p5_sc;         // 1x1 shortcut folded into the block2 p5 conv: 0 off, 1 auto, 2 always ("p5_sc")
+extern int g_p5_dist;       // p5 split-K combine by every slice where the grid is co-resident: 0 off, 1 on ("p5_dist")
 extern int g_spin_bound;     // polls before an in-kernel hand-off wait fails: ITSD_ERR_HANDOFF ("spin_bound", diagnostic)
 extern int g_attn_split;     // attn_block_split_kernel at small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")
@@ -168,6 +169,12 @@ struct ConvArgs {
   const void* sc_src2;
   int sc_C1, sc_C2, sc_split;
   const void* sc_wfrag;
+  // conv3x3_gn_p5_kernel's split-K combine shared by all slices (kdist != 0: every block runs one item, so the
+  // grid is co-resident): each slice waits for the tile's other slices and finishes its own share of the tile's
+  // units; a wait that exhausts spin_bound polls sets bit 1 of *err and writes NaN (ITSD_ERR_HANDOFF)
+  int kdist;
+  int* err;
+  int spin_bound;
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -66,6 +66,8 @@ int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's 
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_p5_sc = 1;         // the ResBlock's 1x1 shortcut folded into its block2 p5 conv: 0 off, 1 auto (cost model), 2 always
+int g_p5_dist = 1;       // p5's split-K combine shared by every slice of a tile where all items are co-resident (2: the
+                         // same plans, combined by the last arriver)
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
 
 __device__ __forceinline__ int swz(int r, int c) { return r * ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -2877,7 +2879,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       for (int j = 0; j < 4; ++j) acc[j] += acc2[j];
 #endif
       TL(2);
-      // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines
+      // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines (or every slice its own units)
       const int tile = tc * nTP + tp;
       if (ST > 1) {
         // Guideline 16's R1 hand-off, per wave: the partial is stored write-through (sc1), the wave
@@ -2897,6 +2899,152 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
                       __float_as_uint(acc[j][4 * g + 3])},
                 slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.kdist) {
+          // ---- the combine shared by all ST slices (every block runs one item: the grid is co-resident). The wave's
+          // 16 (pixel block j, cout group g) units of 32 px x 8 couts form NU statistics units of NJ pixel blocks (one
+          // consumer GroupNorm slot each: W = 4 a half block, W = 8 a pair, W >= 16 the tile); slice z finishes units
+          // u = z, z + ST, ... (u = jg * 4 + g, j = jg NJ + jj): it waits until all ST partials of its (tile, wave) are
+          // stored, sums each unit's ST partials in slice order and runs the epilogue for those units. Counter (one
+          // 128-B line per (tile, wave): 512 waves polling a few shared lines serialise at their memory channel):
+          // arrivals in the low 16 bits, departures in the high ones; the last departure resets it to 0 (the tickets
+          // are zero between launches, as with the last-arriver form). One slab round trip per 8 KB instead of ST
+          // serial ones in one block (30 us of a 56 us 4x4 launch at N = 32, ST = 8: profiles/r05/
+          // p5_timeline_n32_r05am.txt). Bit-identical to the last-arriver combine: the same slice order, the same
+          // statistics tree (per lane over j, then lane pairs by bits 16 / 8 / 4 / 2 / 1 of the pixel lane). (The
+          // unrolled epilogue below with per-unit store / statistics masks instead measured slower: its register
+          // pressure spilled the staging, profiles/r06/p5_timeline_n32_shared_r06c.txt.)
+          constexpr int NJ = W == 4 ? 1 : W == 8 ? 2 : 4, NU = 16 / NJ;
+          int* const tk = a.tickets + (tile * 4 + wid) * 32;  // (tiles x 4 x 32 <= kTicketCap: p5_dist)
+          const int nown = z < NU ? (NU - 1 - z) / ST + 1 : 0;
+          if (nown == 0) {  // (ST > NU: no unit of its own) arrive and depart at once
+            if (lane == 0) __hip_atomic_fetch_add(tk, 0x10001, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            TL(3);
+            return;  // (the block's only item: nothing, such as the A ring, stays live)
+          }
+          int bad = 0;
+          if (lane == 0) {
+            int v = (__hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffff) + 1;
+            TL(3);
+            for (int it = 0; v < ST && it < a.spin_bound; ++it) {  // bounded: a grid that is not co-resident cannot hang
+              __builtin_amdgcn_s_sleep(2);
+              v = __hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffff;
+            }
+            bad = v < ST;
+            if (bad) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          bad = __builtin_amdgcn_readfirstlane(bad);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+          TL(4);  // (timeline, shared combine: 3 partial drained + arrived, 4 every slice arrived, 5 done)
+          // staging: the slab loads land in registers (sc1) and go through this wave's 16 KB of free LDS (halo buffers
+          // for waves 0 / 1, the unused residual tile for 2 / 3), so that runtime (fragment, slice) slots map to
+          // static registers
+          char* const stg = wid < 2 ? smem + wid * 16384 : rres + RTILE + (wid - 2) * 16384;
+          static_assert(2 * HALO >= 2 * 16384, "p5 combine staging");
+          const int tileP = tp * 128, tileC = tc * CONV_BM;
+          const int nfrag = nown * NJ, F = 16 / ST;  // fragments (unit, jj) of this wave; a batch of F x ST slots
+          f32x4 s4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
+          // lane exchange with lane ^ w (as the last-arriver epilogue's statistics: DPP within a row, else swizzle)
+          auto xchg = [](float x, auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const int xi = __builtin_bit_cast(int, x);
+            int r;
+            if constexpr (w == 1) r = __builtin_amdgcn_update_dpp(0, xi, 0xB1, 0xF, 0xF, false);
+            else if constexpr (w == 2) r = __builtin_amdgcn_update_dpp(0, xi, 0x4E, 0xF, 0xF, false);
+            else if constexpr (w == 8) r = __builtin_amdgcn_update_dpp(0, xi, 0x128, 0xF, 0xF, false);
+            else r = __builtin_amdgcn_ds_swizzle(xi, 0x1F | (w << 10));
+            return __builtin_bit_cast(float, r);
+          };
+          auto bfly = [&](auto wc) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s4[e] += xchg(s4[e], wc);
+              q4[e] += xchg(q4[e], wc);
+            }
+          };
+          for (int f0 = 0; f0 < nfrag; f0 += F) {
+            const int nl = std::min(F, nfrag - f0) * ST;
+            int fr = f0, sl = 0;  // the next slot's fragment and slice (uniform, advanced slot by slot)
+            auto slot_off = [&]() __attribute__((always_inline)) {
+              const int u = z + ST * (fr / NJ), jj = fr - (fr / NJ) * NJ;
+              const int j = (u >> 2) * NJ + jj, g = u & 3;
+              const uint32_t o = wbase + sl * zstride + (uint32_t)(j * 4 + g) * 1024;
+              if (++sl == ST) { sl = 0; ++fr; }
+              return o;
+            };
+            // 8 registers: the second 8 slots' loads go out as the first 8 are written (two overlapped round trips;
+            // 16 registers spilled the kernel)
+            u32x4 vv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if (i < nl) vv[i] = __builtin_amdgcn_raw_buffer_load_b128(slab, slot_off(), 0, 16);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              if (i < nl) *(u32x4*)(stg + i * 1024 + lane * 16) = vv[i];
+              if (i + 8 < nl) vv[i] = __builtin_amdgcn_raw_buffer_load_b128(slab, slot_off(), 0, 16);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if (i + 8 < nl) *(u32x4*)(stg + (i + 8) * 1024 + lane * 16) = vv[i];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int f = 0; f < nl / ST; ++f) {
+              const int frg = f0 + f, u = z + ST * (frg / NJ), jj = frg - (frg / NJ) * NJ;
+              const int j = (u >> 2) * NJ + jj, g = u & 3;
+              const char* p = stg + (f * ST) * 1024 + lane * 16;
+              f32x4 x = *(const f32x4*)p;
+              for (int s2 = 1; s2 < ST; ++s2) x += *(const f32x4*)(p + s2 * 1024);
+              // epilogue of fragment (j, g): lane = pixel 32 j + rl, couts c .. c + 3
+              const int pl = j * 32 + rl, seg = pl / SPX, c = wid * 32 + 8 * g + 4 * hh;
+              const bool live = Cf::ROWS ? tp * 128 < a.M : tp * NSEG + seg < nimg;
+              const f32x4 ad = *(const f32x4*)(addv + seg * CONV_BM + c);
+              uint2 rr = *(const uint2*)(rres + pl * 256 + ((((c >> 3) ^ pl) & 15) << 4) + 8 * hh);
+              if (a.resid == nullptr) rr = uint2{0u, 0u};
+              const float nan = __builtin_nanf("");
+              const T b0 = f2bf(bad ? nan : x[0] + ad[0] + __uint_as_float(rr.x << 16));
+              const T b1 = f2bf(bad ? nan : x[1] + ad[1] + __uint_as_float(rr.x & 0xffff0000u));
+              const T b2 = f2bf(bad ? nan : x[2] + ad[2] + __uint_as_float(rr.y << 16));
+              const T b3 = f2bf(bad ? nan : x[3] + ad[3] + __uint_as_float(rr.y & 0xffff0000u));
+              if (live)
+                *(uint2*)((T*)a.out + (size_t)(tileP + pl) * a.Cout + tileC + c) =
+                    uint2{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+              const float m = live ? 1.0f : 0.0f;
+              const float r0 = bf2f(b0) * m, r1 = bf2f(b1) * m, r2 = bf2f(b2) * m, r3 = bf2f(b3) * m;
+              s4[0] += r0; q4[0] = fmaf(r0, r0, q4[0]);
+              s4[1] += r1; q4[1] = fmaf(r1, r1, q4[1]);
+              s4[2] += r2; q4[2] = fmaf(r2, r2, q4[2]);
+              s4[3] += r3; q4[3] = fmaf(r3, r3, q4[3]);
+              if (jj == NJ - 1) {  // the unit's statistics slot is complete: lane pairs by bits (16) 8 4 2 1 of rl
+                if (a.stats) {
+                  if constexpr (W != 4) bfly(std::integral_constant<int, 16>{});
+                  bfly(std::integral_constant<int, 8>{});
+                  bfly(std::integral_constant<int, 4>{});
+                  bfly(std::integral_constant<int, 2>{});
+                  bfly(std::integral_constant<int, 1>{});
+                  if (W == 4) {
+                    const int img = tp * NSEG + 2 * j + (rl >> 4);
+                    if ((rl & 15) == 0 && img < nimg) {
+                      *(f32x4*)(a.stats + ((long long)img * 2) * a.Cout + tileC + c) = s4;
+                      *(f32x4*)(a.stats + ((long long)img * 2 + 1) * a.Cout + tileC + c) = q4;
+                    }
+                  } else {
+                    const long long slot = W == 8 ? tp * NSEG + (j >> 1) : tp;
+                    if (rl == 0 && slot * (W == 8 ? 64 : 128) < a.M) {
+                      *(f32x4*)(a.stats + (slot * 2) * a.Cout + tileC + c) = s4;
+                      *(f32x4*)(a.stats + (slot * 2 + 1) * a.Cout + tileC + c) = q4;
+                    }
+                  }
+                }
+                s4 = f32x4{0.f, 0.f, 0.f, 0.f};
+                q4 = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+            }
+          }
+          if (lane == 0) {  // depart; the last one resets the counter
+            const int old = __hip_atomic_fetch_add(tk, 0x10000, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((old >> 16) == ST - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          TL(5);
+          return;
+        } else {
         int old = 0;
         if (lane == 0) old = __hip_atomic_fetch_add(a.tickets + tile * 4 + wid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         old = __builtin_amdgcn_readfirstlane(old);
@@ -2915,8 +3063,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
                 acc[j][4 * g + e] = sl == 0 ? __uint_as_float(v[e]) : acc[j][4 * g + e] + __uint_as_float(v[e]);
             }
         }
+        }  // (last arriver)
       }
-      TL(3);
+      if (!a.kdist) TL(3);
       // ---- epilogue: out = acc + addv + residual (lane: pixel 32j + rl, couts 32w + 8g + 4hh + e)
       const int tileP = tp * 128, tileC = tc * CONV_BM;
       const float* av = addv + (k & 1) * NSEG * CONV_BM + wid * 32 + 4 * hh;
@@ -3015,7 +3164,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
         }
       }
-      TL(4);
+      if (!a.kdist) TL(4);
     }
     TL(5);
     return;
@@ -3571,18 +3720,29 @@ int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false) {
 // conv3x3_gn_p5_kernel: levels whose 128-pixel tiles hold whole images
 bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 || W == 32 || W == 64); }
 
+// The split-K combine shared by every slice (ConvArgs::kdist): where every item has a block of its own (the grid
+// co-resident), 3 to 16 slices (arrival count in 16 bits, one 16-slot staging batch a fragment; at 2 slices it measured
+// +1 % at N = 256, whose 4x4 launches move 2 x 8 MB of partials: the last arriver's two serial reads cost no more than
+// the shared form's poll and staging, profiles/r06/stepab_a256_r06b.txt). g_p5_dist 2: planned
+// as shared, combined by the last arriver (the parity tests' bit-identity reference for the same plan)
+static bool p5_dist(int tiles, int st) {
+  return g_p5_dist && st > 2 && st <= 16 && (long long)tiles * st <= g_num_cus && (long long)tiles * 4 * 32 <= kTicketCap;
+}
+// its cost in chunk-times: the last-arriving slice reads all S partials serially (~0.3 a slice); shared, one slab
+// round trip a slice and the epilogue spread over the slices
+static double p5_combine_cost(int tiles, int st) { return st <= 1 ? 0.0 : p5_dist(tiles, st) ? 0.6 : 0.3 * st; }
+
 // K slices of a p5 launch: the S minimising ceil(items / CUs) x (chunks per slice + ~1.5 chunks of
-// prologue / epilogue / combine), bounded by the slab and ticket capacities
+// prologue / epilogue) + the combine, bounded by the slab and ticket capacities
 static int p5_split(const ConvArgs& a, int tiles, int nch) {
   int S = 1;
   if (g_p5_split > 0) {
     S = std::min(g_p5_split, nch);
   } else {
     double best = 1e30;
-    // (the last arriving slice of a tile reads all S partials: ~0.3 chunk-times a slice)
     for (int s = 1; s <= std::min(nch, 16); ++s) {
       const double waves = std::ceil((double)tiles * s / g_num_cus);
-      const double cost = waves * (std::ceil((double)nch / s) + 1.5) + (s > 1 ? 0.3 * s : 0.0);
+      const double cost = waves * (std::ceil((double)nch / s) + 1.5) + p5_combine_cost(tiles, s);
       if (cost < best - 1e-9) { best = cost; S = s; }
     }
   }
@@ -3662,7 +3822,7 @@ static int p5_plan(const ConvArgs& a, int* S_out) {
   auto cost = [&](int s, int s2) {
     const double waves = std::ceil((double)tiles * (s + s2) / g_num_cus);
     const double c3 = std::ceil((double)nch / s) + 1.5, c1 = s2 ? 0.4 * std::ceil((double)nchx / s2) + 1.5 : 0.0;
-    return waves * std::max(c3, c1) + (s + s2 > 1 ? 0.3 * (s + s2) : 0.0);
+    return waves * std::max(c3, c1) + p5_combine_cost(tiles, s + s2);
   };
   double best = 1e30;
   int bs = 0, bs2 = 0;
@@ -3695,6 +3855,7 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   a.ksplit = S;
   a.sc_split = S2;
   const int items = tiles * (S + S2);
+  a.kdist = g_p5_dist == 1 && p5_dist(tiles, S + S2);
   const dim3 g(std::min(items, g_num_cus));
   if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p5_kernel<64>, g, dim3(512), 0, s, a);
   else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);

@@ -115,9 +115,11 @@ def test_headline_N256_window_vs_oracle():
     _check_window(ARCH_A, 256, [0, 129, 255], 1000, 10)
 
 
-@pytest.mark.parametrize("n,idx", [(32, [0, 17, 31]), (64, [0, 40, 63]), (1024, [0, 333, 700, 1023])])
+@pytest.mark.parametrize("n,idx", [(8, [0, 5, 7]), (16, [0, 9, 15]), (32, [0, 17, 31]), (64, [0, 40, 63]),
+                                   (1024, [0, 333, 700, 1023])])
 def test_sweep_batches_forward_vs_oracle(n, idx):
-    """The N sweep (north_star N in {64, 256, 1024}; N = 32 is the 8-GPU shard of N = 256): the
+    """The N sweep (north_star N in {64, 256, 1024}; N = 32 is the 8-GPU shard of N = 256, N = 16 / 8 the 4- / 8-GPU
+    shards of N = 64): the
     persistent convs' grids, the split-K small level and the attention grid at each batch."""
     _check_forward(ARCH_A, n, idx, seed=n)
 

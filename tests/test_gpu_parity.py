@@ -662,6 +662,120 @@ def test_p4_96_cout_tiles_bit_identical_n256():
     assert _rel_l2(c96[idx], ref) < REL_L2_BF16
 
 
+@pytest.mark.parametrize("n", [16, 32])
+def test_small_8x8_split_convs_vs_conv_pipe(n):
+    """Small batches: the 8x8 level's plain convs whose 128x128 conv_pipe grid under-fills the chip run on
+    conv_small's 64x64 whole-image tiles (option small_8x8), K split in-launch where a slice keeps >= small_minks
+    K-chunks (shipped 8: these K = 2304 convs run whole, the same k order as conv_pipe; at 2 they split). Since
+    round 5 the ResBlock shortcuts are folded into their block2 p5 conv, so at these batches the convs left on this
+    path are the 16x16 -> 8x8 DownSample (3x3 s2) -- the census pins it, and that no 8x8 1x1 conv remains.
+    Deterministic, within 1e-2 relative L2 of conv_pipe (small_8x8 = 0), bf16 bound vs oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(680 + n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    small8 = [o for o in ops if o["kind"] == "conv" and o["H"] == 8 and "conv_small" in o["kernel"]]
+    assert small8 and all(o["ks"] == 3 for o in small8), [(o["ks"], o["K"], o["kernel"]) for o in small8]
+    assert not any(o["kind"] == "conv" and o["H"] == 8 and o["ks"] == 1 for o in ops)  # (shortcuts folded)
+
+    def run(v, m=8):
+        rt.set_option("small_8x8", v)
+        rt.set_option("small_minks", m)
+        try:
+            return net(x.cuda(), t.cuda()).float().cpu()
+        finally:
+            rt.set_option("small_8x8", 1)
+            rt.set_option("small_minks", 8)
+
+    w = run(1)
+    assert torch.equal(w, run(1))
+    ws = run(1, 2)
+    assert torch.equal(ws, run(1, 2))
+    p = run(0)
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    d, ds, e = _rel_l2(w, p), _rel_l2(ws, p), _rel_l2(w[idx], ref)
+    print(f"n={n}: 8x8 conv_small vs conv_pipe rel-L2 {d:.2e} (split K {ds:.2e}); vs oracle {e:.2e}")
+    assert d < 1e-2 and ds < 1e-2 and e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("n", [16, 32])
+def test_small_wide_stats_free_convs_vs_conv_pipe(n):
+    """Small batches: the statistics-free 1x1 convs of 8x8 .. 32x32 images whose 128x128 conv_pipe grid
+    under-fills the chip run on conv_small's 64x64 tiles (inside one image, split K; option small_wide). With the
+    shortcut fold on (shipped) none is left at these batches -- the census pins that -- so the path is exercised
+    with the fold off (p5_sc 0: the 15 ResBlock shortcuts, the form the fold's cost model falls back to where the
+    extra slices cost more than the launch): deterministic, within 1e-2 relative L2 of conv_pipe (small_wide = 0)
+    and within the bf16 bound of the oracle."""
+    a = ARCH_A
+    net = _net(a, "bf16")
+    gen = torch.Generator().manual_seed(660 + n)
+    x = torch.randn(n, 3, 32, 32, generator=gen)
+    t = torch.randint(0, a.T, (n,), generator=gen)
+    ops = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda())
+    assert not any(o["kind"] == "conv" and o["H"] >= 8 and o["ks"] == 1 for o in ops)  # (all folded)
+
+    def run(v, census=False):
+        rt.set_option("small_wide", v)
+        rt.set_option("p5_sc", 0)
+        try:
+            o = net.native(n).profile_ops(x.cuda(), t.to(torch.int32).cuda()) if census else None
+            return net(x.cuda(), t.cuda()).float().cpu(), o
+        finally:
+            rt.set_option("small_wide", 1)
+            rt.set_option("p5_sc", 1)
+
+    w, ops0 = run(1, census=True)
+    wide = [o for o in ops0 if o["kind"] == "conv" and o["H"] >= 8 and o["ks"] == 1 and "conv_small" in o["kernel"]]
+    assert len(wide) >= 10, [(o["H"], o["K"], o["kernel"]) for o in ops0 if o["ks"] == 1]
+    assert torch.equal(w, run(1)[0])
+    p = run(0)[0]
+    idx = [0, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
+    d, e = _rel_l2(w, p), _rel_l2(w[idx], ref)
+    print(f"n={n}: conv_small (wide) vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_dead_tap_pruning_archC_1x1_level(precision):
+    """Arch C's 1x1 level (ModelCondition.py: ch_mult [1, 4, 8, 8, 4, 2] at 32 px): taps that read only padding for
+    every output pixel are dropped at build time (option tap_prune) -- the 3x3 convs on 1x1 images run their centre
+    tap (ks 1), the DownSample 2x2 -> 1x1 (c1 3x3 + c2 5x5, stride 2, merged into one 5x5 conv at build time, option
+    down_merge) a 2x2 window, the ConvTranspose from the 1x1 grid its centre tap per phase. Exact in arithmetic (the
+    dropped taps multiply zero padding): the census shows no 3x3+ conv left at H = 1 and exactly one merged
+    DownSample, and a guided batch (2N = 64, the C3 leg's) matches the oracle (fp32 max|d| <= 2e-4, bf16 rel-L2
+    <= 2e-2)."""
+    a = ARCH_C
+    net = _net(a, precision)
+    n = 64
+    gen = torch.Generator().manual_seed(641)
+    xc = torch.randn(n, 3, 32, 32, generator=gen)
+    tc = torch.randint(0, a.T, (n,), generator=gen)
+    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n // 2, dtype=torch.long)])
+    x, t, lb = xc.cuda(), tc.cuda(), lab.cuda()
+    ops = net.native(n).profile_ops(x, t.to(torch.int32))
+    h1 = [o for o in ops if o["kind"] == "conv" and o["H"] == 1]
+    assert h1 and all(o["ks"] <= 2 for o in h1), [(o["ks"], o["K"], o["kernel"]) for o in h1]
+    assert sum(o["ks"] == 2 for o in h1) == 1  # the DownSample into the 1x1 level (c1 + c2 as one 5x5 s2 conv)
+    eps = net(x, t, lb).float().cpu()
+    idx = [0, 31, 32, n - 1]
+    with torch.no_grad():
+        ref = _oracle(a, synthetic_state_dict(a, 0))(xc[idx], tc[idx], lab[idx])
+    if precision == "fp32":
+        d = (eps[idx] - ref).abs().max().item()
+        print(f"Arch C 2N=64 fp32 (pruned taps) max|d| vs oracle {d:.2e}")
+        assert d <= EPS_TOL_FP32
+    else:
+        e = _rel_l2(eps[idx], ref)
+        print(f"Arch C 2N=64 bf16 (pruned taps, LDS-staged flash attention) rel-L2 vs oracle {e:.2e}")
+        assert e < REL_L2_BF16
+
+
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-5), ("bf16", 1e-2)])
 def test_one_token_attnblock_fold_archC(precision, tol):
     """Arch C's 1x1-level AttnBlocks (ModelCondition.py, one token): the softmax over a single key is exactly 1,
