@@ -139,7 +139,8 @@ def conv_alg_bytes(o) -> float:
     """Algorithmic HBM bytes of one bf16 conv launch, every operand once: input activations, weights,
     output, the residual operand when the op adds one (ResBlock block2 / shortcut sums, Model.py:184),
     the output's GroupNorm statistics slab (fp32 sum and square sum per channel and slot of
-    min(HW, 128) pixels) and, for a fused GroupNorm+SiLU input, the input's statistics slab read."""
+    min(HW, 128) pixels), for a fused GroupNorm+SiLU input the input's statistics slab read, and for a
+    folded 1x1 shortcut (K slices of the block2 conv) the shortcut's input and weights."""
     ks = max(1, o["ks"])
     cin = o["K"] // (ks * ks)
     su = o["stride_up"]
@@ -154,6 +155,8 @@ def conv_alg_bytes(o) -> float:
     if o.get("gn_in"):
         hw_in = hw_out * stride * stride if not ups else hw_out // 4
         b += 4.0 * 2 * (m_in / min(hw_in, 128)) * cin
+    if o.get("sc_cin"):  # a ResBlock 1x1 shortcut folded in as K slices: its input and weights (no residual operand)
+        b += 2.0 * (o["M"] * o["sc_cin"] + o["N"] * o["sc_cin"])
     return b
 
 

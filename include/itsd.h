@@ -177,19 +177,23 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
 int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int op_index, int reps, double* ms,
                     void* stream);
 
-/* Process-wide switches for A/B measurements (api.hip lists every key): kernel variants and
- * tile choices ("conv_variant", "splitk", "small_conv", "gn_wide", "fuse_gn", "io_mfma",
- * "p4_sub", "p4_plain", "p5", "p5_split", "p5_sc", "gn_fold", "attn_split", "attn_wide", "attn_wide_nq",
- * "conv1x1", "small_wide", "small_8x8", "subpix_split", "convt_prune", "small_minks"; build-time, read at create: "attn_fuse",
- * "tap_prune", "down_merge") and measurement-only ablations ("conv_dbg"). Defaults are the shipped
- * choices; every alternative is covered by a parity test. */
+/* Process-wide choices between the shipped paths (api.hip lists every key and its range): kernel and tile
+ * choices ("conv_variant", "splitk" 0/1, "splitk_inl", "small_conv", "gn_wide", "fuse_gn", "io_mfma", "p4_w",
+ * "p4_sub", "p4_plain", "p4_c96", "p5", "p5_split", "p5_sc", "p5_dist", "gn_fold", "attn_split", "attn_wide",
+ * "attn_wide_nq", "conv1x1" 0/1, "small_wide", "small_8x8", "subpix_split", "convt_prune"), the in-kernel hand-off
+ * poll bound ("spin_bound"), and build-time choices read at create ("attn_fuse", "attn_s1", "tap_prune",
+ * "down_merge"). Defaults are the shipped choices; every alternative is covered by a parity test. Measurement
+ * switches of measured-and-dropped variants ("conv_dbg", "attn_cs", "attn_aq", "p4_xcd", "small_minks", forced
+ * "splitk" slice counts, "conv1x1" 2) exist in diagnostic builds only (tools/build_diag.sh): this library returns
+ * ITSD_ERR_INVALID for them. */
 int itsd_set_option(const char* key, int value);
 
 /* Introspection of a handle (no device work): "graph_captures" (step graphs captured and
  * instantiated so far; a search replays one graph across all its rounds), "max_batch",
  * "T_sched", "ws_bytes" (activation arena), "ops" (program length); and, synchronising the
  * handle's stream, "status" = the in-kernel hand-off status word of the last forward / sampler run
- * (0 ok; bit 0: attn_block_split_kernel's wait exhausted its bound -- ITSD_ERR_HANDOFF). */
+ * (0 ok; bit 0: attn_block_split_kernel's wait exhausted its bound, bit 1: conv3x3_gn_p5_kernel's shared split-K
+ * combine -- ITSD_ERR_HANDOFF). */
 int itsd_unet_query(const itsd_unet* u, const char* key, int64_t* value);
 
 /* Name of census kernel id `id` (itsd_profile_ops): the launch site's kernel expression,

@@ -1121,7 +1121,12 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
       const int segs = u->bf16 ? conv_gn_wide_segs(out.H, out.W, c.nb * out.H * out.W, o.Cout) : 0;
       kind = segs == 1 ? kCensusConvGNW : segs == 4 ? kCensusConvGNW4 : kCensusConvGN;
     }
-    CHK(mark(kind, op_flops(u, o, c.nb), [&]() { return launch_op(u, o, c, s); }));
+    double fl = op_flops(u, o, c.nb);
+    if (c.census && o.kind == OP_CONV && o.sc_op >= 0) {  // + the folded shortcut's K slices (1x1, its Cin)
+      ConvArgs na{};
+      if (conv_args(u, o, c, na) == ITSD_OK && na.sc_C1 + na.sc_C2 > 0) fl += 2.0 * na.M * (double)o.Cout * (na.sc_C1 + na.sc_C2);
+    }
+    CHK(mark(kind, fl, [&]() { return launch_op(u, o, c, s); }));
   }
   // tail GN + conv (+ sampler update); bf16 MFMA tail: GN coefficients, then one fused launch
   cur_op = 0;
@@ -1239,6 +1244,16 @@ const char* itsd_kernel_name(int id) {
 
 int itsd_set_option(const char* key, int value) {
   if (!key) return fail(ITSD_ERR_INVALID, "null key");
+#ifndef ITSD_DIAG
+  // (round 6) measurement switches -- the conv_dbg ablations, forced attention tilings, the XCD tile
+  // order at every level, conv_small's slice floor, forced split-K slice counts and the 7-stage 1x1 ring -- select
+  // measured-and-dropped variants: diagnostic builds only (tools/build_diag.sh). The shipped library takes the
+  // shipped choices below (auto / off / forced forms of the paths it ships, each A/B'd by a parity test).
+  for (const char* dk : {"conv_dbg", "attn_cs", "attn_aq", "p4_xcd", "small_minks"})
+    if (!std::strcmp(key, dk)) return fail(ITSD_ERR_INVALID, std::string(key) + ": diagnostic builds only (tools/build_diag.sh)");
+  if (!std::strcmp(key, "splitk") && value > 1) return fail(ITSD_ERR_INVALID, "splitk in [0,1] (forced slice counts: diagnostic builds)");
+  if (!std::strcmp(key, "conv1x1") && value > 1) return fail(ITSD_ERR_INVALID, "conv1x1 in [0,1] (the 7-stage ring: diagnostic builds)");
+#endif
   ++itsd::g_option_gen;  // cached step graphs baked in the previous kernel choices
   if (!std::strcmp(key, "conv_variant")) {  // 2: conv_pipe (shipped); 1: conv_igemm (register-staged, parity checks)
     if (value < 1 || value > 2) return fail(ITSD_ERR_INVALID, "conv_variant in [1,2]");
@@ -1855,6 +1870,10 @@ int itsd_profile_ops(itsd_unet* u, const float* x, const int32_t* t, int n, int 
         // flags for the algorithmic-bytes count (bench.py conv_alg_bytes): bit 0 a residual operand, bit 1 the
         // output's GroupNorm statistics written, bit 2 the input GroupNorm(+SiLU) fused (its statistics read)
         sh[7] = (o.resid >= 0 ? 1 : 0) | (out.stats != SIZE_MAX ? 2 : 0) | (o.coef != SIZE_MAX ? 4 : 0);
+        if (o.kind == OP_CONV && o.sc_op >= 0) {  // a block2 conv with its 1x1 shortcut folded in as K slices: no
+          ConvArgs na{};                          // residual operand; the shortcut's input channels in bits 8..
+          if (conv_args(u, o, c, na) == ITSD_OK && na.sc_C1 + na.sc_C2 > 0) sh[7] = (sh[7] & ~1) | ((na.sc_C1 + na.sc_C2) << 8);
+        }
       }
     }
     ++k;

@@ -150,7 +150,10 @@ int calibrate_run(int what, double* value, hipStream_t s) {
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
-  if (!rc && hipGetLastError() != hipSuccess) rc = ITSD_ERR_HIP;
+  // (read and cleared on every path: a failed hipMalloc leaves hipErrorOutOfMemory as this thread's last error, which
+  // the next launch_* helper would report as its own kernel-launch failure)
+  const hipError_t last = hipGetLastError();
+  if (!rc && last != hipSuccess) rc = ITSD_ERR_HIP;
   *value = best;
   return rc;
 }

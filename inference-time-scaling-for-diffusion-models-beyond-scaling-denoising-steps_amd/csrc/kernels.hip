@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
   // ---- 4. out = x + O Wp^T + bp for this block's output channels; statistics of its channels
   float* const spart = (float*)(sm + R_ST);  // [token block][2][CW]
   bf16_t* out = a.out + (size_t)img * S * C;
-  const float poison = hbad ? __builtin_nanf("") : 0.0f;  // (a failed hand-off: NaN outputs, see handoff)
+  const bool hb = hbad != 0;  // (a failed hand-off, see handoff: NaN outputs)
   for (int cbl = w; cbl < CBg; cbl += 8) {  // (CBg <= 6: one unit a wave, its fragments loaded above)
     const int cb = g * CBg + cbl;
     f32x16 acc[2];
@@ -1028,10 +1028,11 @@ __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs 
         const int c = 32 * cb + 8 * q + 4 * hh;
         const f32x4 bb = *(const f32x4*)(a.bp + c);
         const uint2 rr = *(const uint2*)(x + (size_t)tk * C + c);
-        const float v0 = acc[tb][4 * q + 0] + bb[0] + poison + __uint_as_float(rr.x << 16);
-        const float v1 = acc[tb][4 * q + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
-        const float v2 = acc[tb][4 * q + 2] + bb[2] + __uint_as_float(rr.y << 16);
-        const float v3 = acc[tb][4 * q + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
+        const float nan = __builtin_nanf("");  // (a failed hand-off: every output channel NaN)
+        const float v0 = hb ? nan : acc[tb][4 * q + 0] + bb[0] + __uint_as_float(rr.x << 16);
+        const float v1 = hb ? nan : acc[tb][4 * q + 1] + bb[1] + __uint_as_float(rr.x & 0xffff0000u);
+        const float v2 = hb ? nan : acc[tb][4 * q + 2] + bb[2] + __uint_as_float(rr.y << 16);
+        const float v3 = hb ? nan : acc[tb][4 * q + 3] + bb[3] + __uint_as_float(rr.y & 0xffff0000u);
         wv[q][0] = pk_bf16(v0, v1);
         wv[q][1] = pk_bf16(v2, v3);
         const float r0 = __uint_as_float(wv[q][0] << 16), r1 = __uint_as_float(wv[q][0] & 0xffff0000u);

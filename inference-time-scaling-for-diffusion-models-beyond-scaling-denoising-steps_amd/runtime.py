@@ -235,7 +235,8 @@ class NativeUNet:
         return [{"kind": dec[i][0], "kernel": dec[i][1], "ms": float(ms[i]), "flops": float(fl[i]),
                  "M": int(sh[i, 0]), "N": int(sh[i, 1]), "K": int(sh[i, 2]), "H": int(sh[i, 3]),
                  "ks": int(sh[i, 4]), "stride_up": int(sh[i, 5]), "op": int(sh[i, 6]),
-                 "resid": bool(sh[i, 7] & 1), "stats_out": bool(sh[i, 7] & 2), "gn_in": bool(sh[i, 7] & 4)}
+                 "resid": bool(sh[i, 7] & 1), "stats_out": bool(sh[i, 7] & 2), "gn_in": bool(sh[i, 7] & 4),
+                 "sc_cin": int(sh[i, 7]) >> 8}
                 for i in range(k)]
 
 

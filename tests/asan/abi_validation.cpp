@@ -66,6 +66,16 @@ int main() {
   expect("set_option gn_reg=4 (removed)", itsd_set_option("gn_reg", 4), ITSD_ERR_INVALID);
   expect("set_option conv_wide=0 (removed)", itsd_set_option("conv_wide", 0), ITSD_ERR_INVALID);
   expect("set_option p4_m16=1 (removed)", itsd_set_option("p4_m16", 1), ITSD_ERR_INVALID);
+  // round 6: measurement switches are diagnostic-build only
+  expect("set_option conv_dbg=1 (diagnostic)", itsd_set_option("conv_dbg", 1), ITSD_ERR_INVALID);
+  expect("set_option attn_cs=2 (diagnostic)", itsd_set_option("attn_cs", 2), ITSD_ERR_INVALID);
+  expect("set_option attn_aq=32 (diagnostic)", itsd_set_option("attn_aq", 32), ITSD_ERR_INVALID);
+  expect("set_option p4_xcd=1 (diagnostic)", itsd_set_option("p4_xcd", 1), ITSD_ERR_INVALID);
+  expect("set_option small_minks=2 (diagnostic)", itsd_set_option("small_minks", 2), ITSD_ERR_INVALID);
+  expect("set_option splitk=2 (diagnostic)", itsd_set_option("splitk", 2), ITSD_ERR_INVALID);
+  expect("set_option conv1x1=2 (diagnostic)", itsd_set_option("conv1x1", 2), ITSD_ERR_INVALID);
+  expect("set_option p5_dist=3", itsd_set_option("p5_dist", 3), ITSD_ERR_INVALID);
+  expect("set_option p5_dist=1", itsd_set_option("p5_dist", 1), ITSD_OK);
   expect("set_option conv_variant=3 (removed)", itsd_set_option("conv_variant", 3), ITSD_ERR_INVALID);
   expect("set_option conv_variant=2 (default)", itsd_set_option("conv_variant", 2), ITSD_OK);
   expect("set_option spin_bound=-1", itsd_set_option("spin_bound", -1), ITSD_ERR_INVALID);
@@ -80,8 +90,8 @@ int main() {
   expect("set_option small_minks=0", itsd_set_option("small_minks", 0), ITSD_ERR_INVALID);
   expect("set_option attn_fuse=2 (removed)", itsd_set_option("attn_fuse", 2), ITSD_ERR_INVALID);
   expect("set_option attn_fuse=1 (default)", itsd_set_option("attn_fuse", 1), ITSD_OK);
-  expect("set_option small_minks=8 (default)", itsd_set_option("small_minks", 8), ITSD_OK);
-  expect("set_option conv_dbg=0", itsd_set_option("conv_dbg", 0), ITSD_OK);
+  expect("set_option small_minks=8 (diagnostic)", itsd_set_option("small_minks", 8), ITSD_ERR_INVALID);
+  expect("set_option conv_dbg=0 (diagnostic)", itsd_set_option("conv_dbg", 0), ITSD_ERR_INVALID);
   {  // a long key: the error message copies it
     std::string k(4096, 'k');
     expect("set_option 4 KiB key", itsd_set_option(k.c_str(), 0), ITSD_ERR_INVALID);

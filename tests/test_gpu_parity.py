@@ -509,36 +509,6 @@ def test_p4_subpixel_convtranspose_vs_conv_pipe_cfg():
     assert d < 1e-2 and e < REL_L2_BF16
 
 
-@pytest.mark.parametrize("arch,n", [(ARCH_A, 32), (ARCH_C, 64)])
-def test_small_split_granularity(arch, n):
-    """conv_small's in-launch split K with >= 8 K-chunks a slice (shipped: fewer, longer slices) against
-    >= 2 (the round-4 start) and >= 1: deterministic, the slices only regroup the fp32 sums (within 1e-2
-    relative L2 of each other), and within the bf16 bound of the oracle."""
-    net = _net(arch, "bf16")
-    gen = torch.Generator().manual_seed(680 + n)
-    xc = torch.randn(n, 3, 32, 32, generator=gen)
-    tc = torch.randint(0, arch.T, (n,), generator=gen)
-    lab = torch.cat([torch.arange(n // 2) % 10 + 1, torch.zeros(n - n // 2, dtype=torch.long)]) if arch.cfg else None
-    args = [xc.cuda(), tc.cuda()] + ([lab.cuda()] if arch.cfg else [])
-
-    def run(m):
-        rt.set_option("small_minks", m)
-        try:
-            return net(*args).float().cpu()
-        finally:
-            rt.set_option("small_minks", 8)
-
-    ship = run(8)
-    assert torch.equal(ship, run(8))
-    d2, d1 = _rel_l2(ship, run(2)), _rel_l2(ship, run(1))
-    idx = [0, n - 1]
-    with torch.no_grad():
-        ref = _oracle(arch, synthetic_state_dict(arch, 0))(xc[idx], tc[idx], *([lab[idx]] if arch.cfg else []))
-    e = _rel_l2(ship[idx], ref)
-    print(f"{arch.kind} n={n}: small_minks 8 vs 2 / 1 rel-L2 {d2:.2e} / {d1:.2e}; vs oracle {e:.2e}")
-    assert d2 < 1e-2 and d1 < 1e-2 and e < REL_L2_BF16
-
-
 def test_convtranspose_live_taps_vs_all_taps():
     """The CFG UpSample's ConvTranspose2d(5, 2, 2, 1) phases on conv3x3_gn_p4_kernel (8x8 -> 16x16 and
     16x16 -> 32x32 at 2N = 64) run only the taps of their 3x3 window that have a kernel tap (9 / 6 / 6 / 4:
@@ -665,8 +635,8 @@ def test_p4_96_cout_tiles_bit_identical_n256():
 @pytest.mark.parametrize("n", [16, 32])
 def test_small_8x8_split_convs_vs_conv_pipe(n):
     """Small batches: the 8x8 level's plain convs whose 128x128 conv_pipe grid under-fills the chip run on
-    conv_small's 64x64 whole-image tiles (option small_8x8), K split in-launch where a slice keeps >= small_minks
-    K-chunks (shipped 8: these K = 2304 convs run whole, the same k order as conv_pipe; at 2 they split). Since
+    conv_small's 64x64 whole-image tiles (option small_8x8), K split in-launch where a slice keeps >= 8 K-chunks
+    (these K = 2304 convs run whole, the same k order as conv_pipe). Since
     round 5 the ResBlock shortcuts are folded into their block2 p5 conv, so at these batches the convs left on this
     path are the 16x16 -> 8x8 DownSample (3x3 s2) -- the census pins it, and that no 8x8 1x1 conv remains.
     Deterministic, within 1e-2 relative L2 of conv_pipe (small_8x8 = 0), bf16 bound vs oracle."""
@@ -680,26 +650,22 @@ def test_small_8x8_split_convs_vs_conv_pipe(n):
     assert small8 and all(o["ks"] == 3 for o in small8), [(o["ks"], o["K"], o["kernel"]) for o in small8]
     assert not any(o["kind"] == "conv" and o["H"] == 8 and o["ks"] == 1 for o in ops)  # (shortcuts folded)
 
-    def run(v, m=8):
+    def run(v):
         rt.set_option("small_8x8", v)
-        rt.set_option("small_minks", m)
         try:
             return net(x.cuda(), t.cuda()).float().cpu()
         finally:
             rt.set_option("small_8x8", 1)
-            rt.set_option("small_minks", 8)
 
     w = run(1)
     assert torch.equal(w, run(1))
-    ws = run(1, 2)
-    assert torch.equal(ws, run(1, 2))
     p = run(0)
     idx = [0, n - 1]
     with torch.no_grad():
         ref = _oracle(a, synthetic_state_dict(a, 0))(x[idx], t[idx])
-    d, ds, e = _rel_l2(w, p), _rel_l2(ws, p), _rel_l2(w[idx], ref)
-    print(f"n={n}: 8x8 conv_small vs conv_pipe rel-L2 {d:.2e} (split K {ds:.2e}); vs oracle {e:.2e}")
-    assert d < 1e-2 and ds < 1e-2 and e < REL_L2_BF16
+    d, e = _rel_l2(w, p), _rel_l2(w[idx], ref)
+    print(f"n={n}: 8x8 conv_small vs conv_pipe rel-L2 {d:.2e}; vs oracle {e:.2e}")
+    assert d < 1e-2 and e < REL_L2_BF16
 
 
 @pytest.mark.parametrize("n", [16, 32])

@@ -106,12 +106,17 @@ def test_conv_tile_options():
     rt.set_option("spin_bound", 1 << 22)
     with pytest.raises(rt.ItsdError):
         rt.set_option("spin_bound", -1)
-    rt.set_option("conv_dbg", 1)
-    with pytest.raises(rt.ItsdError, match="diagnostic builds only"):
-        rt.set_option("conv_dbg", 4096 | (2 << 13))
+    # (round 6) measurement switches are diagnostic-build only: the shipped ABI refuses them
+    for key, val in (("conv_dbg", 1), ("conv_dbg", 0), ("attn_cs", 2), ("attn_aq", 32), ("p4_xcd", 1),
+                     ("small_minks", 2), ("splitk", 2), ("conv1x1", 2)):
+        with pytest.raises(rt.ItsdError, match="diagnostic build"):
+            rt.set_option(key, val)
+    for key, val in (("splitk", 0), ("splitk", 1), ("conv1x1", 0), ("conv1x1", 1)):  # their shipped values stay
+        rt.set_option(key, val)
     # a refused value leaves the previous setting in place (validated before it is stored)
-    assert rt.lib().itsd_set_option(b"conv_dbg", 1) == 0
-    rt.set_option("conv_dbg", 0)
+    for v in (0, 2, 1):
+        rt.set_option("p5_dist", v)
+    assert rt.lib().itsd_set_option(b"p5_dist", 3) != 0
 
 
 def test_shipped_library_holds_only_product_kernels():

@@ -106,11 +106,52 @@ def bf16_emulation(a, x_T, streams, T, beta_T):
             "score_absdiff_max": max(dscore)}
 
 
+def bf16_emulation_vs_fixture(name, a, beta_T, w=None):
+    """(round 6) C3 / C4: the bf16 emulation's drift over the whole loop against the REFERENCE's own fp32 trajectory
+    (tests/golden/full_<name>.npz, tools/gen_golden_full.py: the reference sampler driven with the same Philox
+    noise) -- the clean fp32 loop is the fixture, so only the emulation runs here. ConvTranspose2d (the CFG UpSample)
+    is rounded like the convolutions."""
+    import torch.nn.functional as F
+    fx = np.load(os.path.join(ROOT, "tests", "golden", f"full_{name}.npz"))
+    x_T, ref = torch.from_numpy(fx["x_T"]), torch.from_numpy(fx["x0"]).double()
+    T, seed, rnd, cands = int(fx["T"]), int(fx["seed"]), int(fx["round"]), [int(c) for c in fx["cands"]]
+    per = int(np.prod(x_T.shape[1:]))
+    run_seed = (seed * 1000003 + rnd) & ((1 << 62) - 1)
+
+    def noise(step, xx):
+        return torch.stack([R.philox_normal(run_seed, step, np.arange(i * per, (i + 1) * per)).reshape(x_T.shape[1:])
+                            for i in cands])
+
+    sd = _sd(a, torch.float32)
+    sdb = {k: (_bf(v) if v.dim() >= 2 else v) for k, v in sd.items()}
+    if w is None:
+        fwb = lambda xx, tt: R.unet_forward(sdb, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
+    else:
+        f3 = lambda xx, tt, ll: R.unet_forward(sdb, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks, labels=ll,
+                                               cfg=True)
+        fwb = R.cfg_eps(f3, torch.full((len(cands),), int(fx["label"])), w)
+    conv2d, convt = F.conv2d, F.conv_transpose2d
+    F.conv2d = lambda x, wt, b=None, *args, **kw: _bf(conv2d(_bf(x), wt, b, *args, **kw))
+    F.conv_transpose2d = lambda x, wt, b=None, *args, **kw: _bf(convt(_bf(x), wt, b, *args, **kw))
+    try:
+        t0 = time.time()
+        with torch.no_grad():
+            emu = R.p_sample_loop(fwb, x_T, R.schedule(1e-4, beta_T, T), noise).double()
+        print(f"  {name} bf16-emulation loop {time.time() - t0:.0f}s", flush=True)
+    finally:
+        F.conv2d, F.conv_transpose2d = conv2d, convt
+    rel = [((emu[i] - ref[i]).norm() / ref[i].norm()).item() for i in range(len(cands))]
+    dscore = [abs(R.oracle_score(emu[i:i + 1].float()) - float(fx["scores"][i])) for i in range(len(cands))]
+    print(f"  {name} bf16 emulation vs the reference: x0 rel-L2 {rel}, score |d| {dscore}", flush=True)
+    return {"images": len(cands), "against": f"tests/golden/full_{name}.npz (the reference's own fp32 loop)",
+            "x0_rel_l2_max": max(rel), "x0_rel_l2_mean": float(np.mean(rel)), "score_absdiff_max": max(dscore)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="short T (smoke of the tool itself)")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden", "tolerance_derivation.json"))
-    ap.add_argument("--only", default="", help="one part (C1c, C1, C2, C5) -> <out>.<part>.json; --merge joins them")
+    ap.add_argument("--only", default="", help="one part (C1c, C1, C2, C5, C3, C4) -> <out>.<part>.json; --merge joins them")
     ap.add_argument("--merge", action="store_true")
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -118,11 +159,28 @@ def main():
     T = 50 if args.quick else 1000
     res = {"factor_fp32": FACTOR_FP32, "factor_bf16": FACTOR_BF16, "T": T}
     parts = {"C1c": "C1c_cfg_fp32_vs_fp64", "C1": "C1_archA_fp32_vs_fp64", "C2": "C2_bf16_emulation",
-             "C5": "C5_bf16_emulation"}
+             "C5": "C5_bf16_emulation", "C3": "C3_bf16_emulation", "C4": "C4_bf16_emulation"}
+    if args.only in ("C3", "C4"):  # (round 6) against the reference fixtures of tools/gen_golden_full.py
+        if args.only == "C3":
+            from itsd.arch import ARCH_C
+            r = bf16_emulation_vs_fixture("C3", ARCH_C, 0.028, w=1.8)
+        else:
+            r = bf16_emulation_vs_fixture("C4", dataclasses.replace(ARCH_A, img_size=64), 0.02)
+        with open(f"{args.out}.{args.only}.json", "w") as fh:
+            json.dump(r, fh, indent=1)
+        return
     if args.merge:
+        # parts measured earlier and not re-run keep their recorded values from the existing JSON
+        prev = {}
+        if os.path.exists(args.out):
+            with open(args.out) as fh:
+                prev = json.load(fh)
         for k, key in parts.items():
-            with open(f"{args.out}.{k}.json") as fh:
-                res[key] = json.load(fh)
+            if os.path.exists(f"{args.out}.{k}.json"):
+                with open(f"{args.out}.{k}.json") as fh:
+                    res[key] = json.load(fh)
+            else:
+                res[key] = prev[key]
         _finish(res, args)
         return
     run = lambda k: not args.only or args.only == k
@@ -182,8 +240,12 @@ def _finish(res, args):
         "FULL_T_BF16_SCORE": FACTOR_BF16 * res["C2_bf16_emulation"]["score_absdiff_max"],
         "C5_BF16_REL_L2": FACTOR_BF16 * res["C5_bf16_emulation"]["x0_rel_l2_max"],
         "C5_BF16_SCORE": FACTOR_BF16 * res["C5_bf16_emulation"]["score_absdiff_max"],
+        "C3_BF16_REL_L2": FACTOR_BF16 * res["C3_bf16_emulation"]["x0_rel_l2_max"],
+        "C3_BF16_SCORE": FACTOR_BF16 * res["C3_bf16_emulation"]["score_absdiff_max"],
+        "C4_BF16_REL_L2": FACTOR_BF16 * res["C4_bf16_emulation"]["x0_rel_l2_max"],
+        "C4_BF16_SCORE": FACTOR_BF16 * res["C4_bf16_emulation"]["score_absdiff_max"],
     }
-    res["command"] = ("python tools/derive_tolerances.py --only <part> (C1c, C1, C2, C5), then --merge"
+    res["command"] = ("python tools/derive_tolerances.py --only <part> (C1c, C1, C2, C5, C3, C4), then --merge"
                       + (" --quick" if args.quick else ""))
     print(json.dumps(res, indent=1))
     if not args.quick:
