@@ -1249,7 +1249,7 @@ int itsd_set_option(const char* key, int value) {
   // order at every level, conv_small's slice floor, forced split-K slice counts and the 7-stage 1x1 ring -- select
   // measured-and-dropped variants: diagnostic builds only (tools/build_diag.sh). The shipped library takes the
   // shipped choices below (auto / off / forced forms of the paths it ships, each A/B'd by a parity test).
-  for (const char* dk : {"conv_dbg", "attn_cs", "attn_aq", "p4_xcd", "small_minks"})
+  for (const char* dk : {"conv_dbg", "attn_cs", "attn_aq", "p4_xcd", "small_minks", "p5_c64"})
     if (!std::strcmp(key, dk)) return fail(ITSD_ERR_INVALID, std::string(key) + ": diagnostic builds only (tools/build_diag.sh)");
   if (!std::strcmp(key, "splitk") && value > 1) return fail(ITSD_ERR_INVALID, "splitk in [0,1] (forced slice counts: diagnostic builds)");
   if (!std::strcmp(key, "conv1x1") && value > 1) return fail(ITSD_ERR_INVALID, "conv1x1 in [0,1] (the 7-stage ring: diagnostic builds)");
@@ -1391,6 +1391,11 @@ int itsd_set_option(const char* key, int value) {
                                        // 1 on, 2 the same plans as 1 combined by the last arriver (bit-identity checks)
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_dist in [0,2]");
     itsd::g_p5_dist = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "p5_c64")) {  // (diagnostic) 64-cout conv3x3_gn_p5_kernel items at 8x8 / 4x4: 0 off, 1 auto, 2 always
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_c64 in [0,2]");
+    itsd::g_p5_c64 = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "gn_fold")) {  // GroupNorm finalize inside conv3x3_gn_p4 / p5_kernel: 0 off, 1 on

@@ -32,6 +32,7 @@ extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 of
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
 extern int g_p5_sc;         // 1x1 shortcut folded into the block2 p5 conv: 0 off, 1 auto, 2 always ("p5_sc")
 extern int g_p5_dist;       // p5 split-K combine by every slice where the grid is co-resident: 0 off, 1 on ("p5_dist")
+extern int g_p5_c64;        // 64-cout p5 items at the 8x8 / 4x4 levels: 0 off, 1 auto, 2 always ("p5_c64", diagnostic)
 extern int g_spin_bound;     // polls before an in-kernel hand-off wait fails: ITSD_ERR_HANDOFF ("spin_bound", diagnostic)
 extern int g_attn_split;     // attn_block_split_kernel at small batches: 0 off, 1 auto, 2/4/6 forced G (itsd_set_option "attn_split")
 extern int g_gn_fold;       // GroupNorm finalize inside p4 / p5 instead of a gn_coef launch (itsd_set_option "gn_fold")

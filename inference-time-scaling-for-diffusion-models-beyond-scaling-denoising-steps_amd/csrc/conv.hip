@@ -2630,10 +2630,16 @@ constexpr int P5_BD = ITSD_P5_BD;    // B fragment buffers (reads two k-steps = 
 // stores, per-slot butterflies over the 16 pixel lanes -- measured N = 256 equal, N = 32 +2.3 %, N = 64 +0.7 %, C4
 // +0.7 % step time against this form, profiles/r05/step_p5_m16_vs_m32.txt: removed)
 
-template <int W>
+// CB (round 6): couts per item, 128 or 64 (W <= 8: a statistics slot never spans the two pixel halves). With 64-cout
+// items waves w and w + 2 share a 32-cout block and each takes two of the four 32-pixel blocks: the same k order per
+// output and the same statistics tree, so the forward is bit-identical to 128-cout items; twice the items at the same
+// K slices -- the 4x4 level at N = 256 fills the 256 CUs without splitting K (128 tiles of 128 couts)
+template <int W, int CB = 128>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   typedef bf16_t T;
   using Cf = Gp5Cfg<W>;
+  static_assert(CB == 128 || (CB == 64 && W <= 8), "p5 cout tile");
+  constexpr int CWB = CB / 32, NJW = CWB;  // 32-cout blocks a tile; 32-pixel blocks a wave (4 waves: CWB x 4 / CWB)
   constexpr int HW = Cf::HW, NSEG = Cf::NSEG, W2 = Cf::W2, HS = Cf::HS, TPS = Cf::TPS, RPP = Cf::RPP;
   constexpr int ITEMS = Cf::ITEMS, HALO = Cf::HALO, TH = Cf::TH, HY0 = Cf::HY0, NHY = Cf::NHY;
   constexpr int SPX = TH * W;  // pixels of one segment
@@ -2665,7 +2671,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Cin = a.C1 + a.C2, nch = Cin / 64, kpt = Cin >> 4;
   const int nimg = a.M / HW, nTP = Cf::ROWS ? a.M / 128 : (nimg + NSEG - 1) / NSEG;
-  const int nTC = a.Cout / CONV_BM, S = a.ksplit;
+  const int nTC = a.Cout / CB, S = a.ksplit;
   // (folded 1x1 shortcut: slices S .. ST-1 run the shortcut's K over its own input, nchx 64-channel chunks)
   const int S2 = a.sc_split, ST = S + S2, nchx = (a.sc_C1 + a.sc_C2) / 64;
   const int NI = nTP * nTC * ST;
@@ -2695,11 +2701,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   if (wid < 4) {
     // ================================================================ MFMA waves
     const int rl = lane & 31, hh = lane >> 5;
-    int hb[4];  // halo row of this lane's pixel (tap 0, 0) in each 32-pixel block
-    int hq[4];  // its swz coordinates SC1 y + SC2 x (W <= 16)
+    const int cw = wid % CWB, jb0 = (wid / CWB) * NJW;  // this wave's 32-cout block and first 32-pixel block
+    int hb[NJW];  // halo row of this lane's pixel (tap 0, 0) in each of its 32-pixel blocks
+    int hq[NJW];  // its swz coordinates SC1 y + SC2 x (W <= 16)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = j * 32 + rl, seg = pl / SPX, rem = pl - seg * SPX, y = rem / W;
+    for (int j = 0; j < NJW; ++j) {
+      const int pl = (jb0 + j) * 32 + rl, seg = pl / SPX, rem = pl - seg * SPX, y = rem / W;
       hb[j] = seg * HS + y * W2 + (rem - y * W);
       hq[j] = SC1 * y + SC2 * (rem - y * W);
     }
@@ -2711,8 +2718,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     // A fragments by buffer loads (conv3x3_gn_p4_kernel's scheme): voffset = this lane's 16 B of the wave's
     // 32-cout block, soffset = the tile's fragment block + chunk + k-step (uniform scalar arithmetic)
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wfrag, (short)0, 0x7fffffff, 0x00020000);
-    const uint32_t avo = (uint32_t)lane * 16 + (uint32_t)wid * ablk;
-    auto abase = [&](int tc, int cc) -> uint32_t { return (uint32_t)(tc * 4) * ablk + (uint32_t)cc * 4 * 1024; };
+    const uint32_t avo = (uint32_t)lane * 16 + (uint32_t)cw * ablk;
+    auto abase = [&](int tc, int cc) -> uint32_t { return (uint32_t)(tc * CWB) * ablk + (uint32_t)cc * 4 * 1024; };
     auto load_a = [&](uint32_t base, int st, u32x4& dst) __attribute__((always_inline)) {
 #if defined(ITSD_DIAG) && defined(P5_AB)
       if constexpr ((P5_AB & 8) != 0) {  // ablation: no A loads
@@ -2722,14 +2729,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #endif
       dst = __builtin_amdgcn_raw_buffer_load_b128(wrs, avo, base + (uint32_t)((st >> 2) * kpt + (st & 3)) * 1024, 0);
     };
-    f32x16 acc[4];
+    f32x16 acc[NJW];
     u32x4 ra[P5_RING];
     // the folded shortcut's A fragments: voffset = this lane's 16 B, soffset = the wave's 32-cout block + chunk + k-step
     const __amdgpu_buffer_rsrc_t wrx = __builtin_amdgcn_make_buffer_rsrc((void*)a.sc_wfrag, (short)0, 0x7fffffff, 0x00020000);
     const uint32_t ablkx = (uint32_t)(nchx * 4) * 1024;
     auto load_ax = [&](int tc, int cc, int st, u32x4& dst) __attribute__((always_inline)) {
       dst = __builtin_amdgcn_raw_buffer_load_b128(wrx, (uint32_t)lane * 16,
-                                                  (uint32_t)(tc * 4 + wid) * ablkx + (uint32_t)(cc * 4 + st) * 1024, 0);
+                                                  (uint32_t)(tc * CWB + cw) * ablkx + (uint32_t)(cc * 4 + st) * 1024, 0);
     };
     bool ring = false;  // ra[0 .. P5_RING-2] hold the next 3x3 item's first k-steps
     {
@@ -2750,13 +2757,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       item_of(k, tp, tc, z);
       const int c0 = chunk_lo(z), c1 = chunk_hi(z);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJW; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
 #if defined(ITSD_DIAG) && defined(P5_CHAINS2)  // diagnostic: 8 accumulation chains (odd k-steps apart)
-      f32x16 acc2[4];
+      f32x16 acc2[NJW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJW; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[j][r] = 0.0f;
 #endif
@@ -2771,20 +2778,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
             for (int st = 0; st < 4; ++st) load_ax(tc, cc + 1, st, ra[4 * (1 - P) + st]);
           }
-          int tx[4];
+          int tx[NJW];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NJW; ++j) {
             const int h = hb[j] + W2 + 1;
             tx[j] = (q & 1) * HALO + h * ROWB + ((hh ^ bunit(j, h, 1, 1)) << 4);
           }
 #pragma unroll
           for (int st = 0; st < 4; ++st) {
-            bf16x8 fx[4];
+            bf16x8 fx[NJW];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) fx[j] = *(const bf16x8*)(smem + (tx[j] ^ (st << 5)));
+            for (int j = 0; j < NJW; ++j) fx[j] = *(const bf16x8*)(smem + (tx[j] ^ (st << 5)));
             const bf16x8 af = __builtin_bit_cast(bf16x8, ra[4 * P + st]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fx[j], acc[j], 0, 0, 0);
+            for (int j = 0; j < NJW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fx[j], acc[j], 0, 0, 0);
           }
           block_sync();  // end of stage q: its halo buffer is free, stage q+1 is published
           ++q;
@@ -2814,13 +2821,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         const char* hcur = smem + (q & 1) * HALO;
         const uint32_t cb = abase(tc, cc);
         const uint32_t nb = cc + 1 < c1 ? abase(tc, cc + 1) : nitem;
-        int tb[4];
-        bf16x8 fb[P5_BD][4];
+        int tb[NJW];
+        bf16x8 fb[P5_BD][NJW];
         auto rd = [&](int st, int buf) __attribute__((always_inline)) {
           if ((st & 3) == 0) {
             const int tap = st >> 2, ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < NJW; ++j) {
               int h = hb[j] + ky * W2 + kx;
               asm volatile("" : "+v"(h));  // rebuilt per tap, not hoisted out of the chunk loop
               tb[j] = (int)(hcur - smem) + h * ROWB + ((hh ^ bunit(j, h, ky, kx)) << 4);
@@ -2829,12 +2836,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #if defined(ITSD_DIAG) && defined(P5_AB)
           if constexpr ((P5_AB & 16) != 0) {  // ablation: no B reads
 #pragma unroll
-            for (int j = 0; j < 4; ++j) fb[buf][j] = bf16x8{(short)(st + j), 0, 0, 0, 0, 0, 0, 1};
+            for (int j = 0; j < NJW; ++j) fb[buf][j] = bf16x8{(short)(st + j), 0, 0, 0, 0, 0, 0, 1};
             return;
           }
 #endif
 #pragma unroll
-          for (int j = 0; j < 4; ++j) fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 3) << 5)));
+          for (int j = 0; j < NJW; ++j) fb[buf][j] = *(const bf16x8*)(smem + (tb[j] ^ ((st & 3) << 5)));
         };
 #pragma unroll
         for (int s0 = 0; s0 < P5_BD - 1; ++s0) rd(s0, s0);
@@ -2847,7 +2854,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           if (step + P5_BD - 1 < 36) rd(step + P5_BD - 1, (step + P5_BD - 1) % P5_BD);
           const bf16x8 af = __builtin_bit_cast(bf16x8, ra[step % P5_RING]);
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NJW; ++j)
 #if defined(ITSD_DIAG) && defined(P5_CHAINS2)
             if (step & 1) acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, fb[step % P5_BD][j], acc2[j], 0, 0, 0);
             else
@@ -2876,7 +2883,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       }  // (3x3 slice)
 #if defined(ITSD_DIAG) && defined(P5_CHAINS2)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += acc2[j];
+      for (int j = 0; j < NJW; ++j) acc[j] += acc2[j];
 #endif
       TL(2);
       // ---- split-K: partial out, ticket; the last slice of this (tile, wave) combines (or every slice its own units)
@@ -2888,10 +2895,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         // write-back / L1 invalidate cost ~2-7 us per episode (MI355X_MICROARCH.md, visibility table)
         const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
             a.splitk_ws, (short)0, (int)std::min<long long>(a.splitk_cap * 4, 0x7fffffffLL), 0x00020000);
-        const uint32_t wbase = (uint32_t)(((size_t)tile * ST * 4 + wid) * 4096 * 4) + lane * 16;
-        const uint32_t zstride = 4 * 4096 * 4;  // bytes between the slices of one (tile, wave)
+        // slab [tile][slice][wave][NJW x 4 KB] (a wave's NJW pixel blocks x 4 cout groups of 1 KB)
+        const uint32_t wbase = (uint32_t)(((size_t)tile * ST * 4 + wid) * NJW * 4096) + lane * 16;
+        const uint32_t zstride = 4 * NJW * 4096;  // bytes between the slices of one (tile, wave)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJW; ++j)
 #pragma unroll
           for (int g = 0; g < 4; ++g)
             __builtin_amdgcn_raw_buffer_store_b128(
@@ -2899,7 +2907,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
                       __float_as_uint(acc[j][4 * g + 3])},
                 slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.kdist) {
+        if (CB == 128 && a.kdist) {
           // ---- the combine shared by all ST slices (every block runs one item: the grid is co-resident). The wave's
           // 16 (pixel block j, cout group g) units of 32 px x 8 couts form NU statistics units of NJ pixel blocks (one
           // consumer GroupNorm slot each: W = 4 a half block, W = 8 a pair, W >= 16 the tile); slice z finishes units
@@ -3054,7 +3062,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         // every slice's partial (this one's included), summed in slice order
         for (int sl = 0; sl < ST; ++sl) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NJW; ++j)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(slab, wbase + sl * zstride + (j * 4 + g) * 1024, 0, 16);
@@ -3067,22 +3075,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
       }
       if (!a.kdist) TL(3);
       // ---- epilogue: out = acc + addv + residual (lane: pixel 32j + rl, couts 32w + 8g + 4hh + e)
-      const int tileP = tp * 128, tileC = tc * CONV_BM;
-      const float* av = addv + (k & 1) * NSEG * CONV_BM + wid * 32 + 4 * hh;
+      const int tileP = tp * 128, tileC = tc * CB;
+      const float* av = addv + (k & 1) * NSEG * CONV_BM + cw * 32 + 4 * hh;
       const bool has_res = a.resid != nullptr;
       float s16[16], q16[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
       const char* rk = rres + (k & 1) * RTILE;  // this item's residual tile (halo waves, before the last barrier)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int pl = j * 32 + rl, seg = pl / SPX;
+      for (int j = 0; j < NJW; ++j) {
+        const int pl = (jb0 + j) * 32 + rl, seg = pl / SPX;
         const bool live = Cf::ROWS ? tp * 128 < a.M : tp * NSEG + seg < nimg;
-        const float* avj = av + seg * CONV_BM;
+        const float* avj = av + seg * CB;
         uint32_t wv[4][2];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int c = wid * 32 + 8 * g + 4 * hh;
+          const int c = cw * 32 + 8 * g + 4 * hh;
           const f32x4 ad = *(const f32x4*)(avj + 8 * g);
           uint2 rr = *(const uint2*)(rk + pl * 256 + ((((c >> 3) ^ pl) & 15) << 4) + 8 * hh);
           if (!has_res) rr = uint2{0u, 0u};
@@ -3110,7 +3118,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             o[d] = sw[0];
             o[2 + d] = sw[1];
           }
-          const int c8 = wid * 32 + 8 * (gp + hh);
+          const int c8 = cw * 32 + 8 * (gp + hh);
           if (live) *(u32x4*)((T*)a.out + (size_t)(tileP + pl) * a.Cout + tileC + c8) = o;
         }
         // consumer GroupNorm statistics: one slot per image (W = 8: j-blocks {0,1} / {2,3};
@@ -3148,16 +3156,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             halve(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
             halve(std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
             halve(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-            const long long slot = W == 8 ? tp * NSEG + (j >> 1) : tp;  // = global pixel / stat_slot_px
-            const int e = rl & 15, co = wid * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
+            const long long slot = W == 8 ? tp * NSEG + ((jb0 + j) >> 1) : tp;  // = global pixel / stat_slot_px
+            const int e = rl & 15, co = cw * 32 + 8 * (e >> 2) + 4 * hh + (e & 3);
             if (slot * (W == 8 ? 64 : 128) < a.M) a.stats[(slot * 2 + (rl >> 4)) * a.Cout + tileC + co] = v[0];
           } else {  // 16-pixel slot = 16 lanes: two values a lane, idx = 2 (rl & 15) + {0, 1}
             halve(std::integral_constant<int, 8>{}, std::integral_constant<int, 32>{});
             halve(std::integral_constant<int, 4>{}, std::integral_constant<int, 16>{});
             halve(std::integral_constant<int, 2>{}, std::integral_constant<int, 8>{});
             halve(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
-            const int img = tp * NSEG + 2 * j + (rl >> 4);
-            const int m = rl & 7, co = wid * 32 + 8 * (m >> 1) + 4 * hh + 2 * (m & 1);
+            const int img = tp * NSEG + 2 * (jb0 + j) + (rl >> 4);
+            const int m = rl & 7, co = cw * 32 + 8 * (m >> 1) + 4 * hh + 2 * (m & 1);
             if (img < nimg) *(float2*)(a.stats + ((long long)img * 2 + ((rl >> 3) & 1)) * a.Cout + tileC + co) = float2{v[0], v[1]};
           }
 #pragma unroll
@@ -3393,8 +3401,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
     int tp, tc, z;
     item_of(k, tp, tc, z);
     const long long trow = a.temb ? (a.temb_tsel ? (long long)(*a.temb_tsel) * a.temb_row_stride : 0) : 0;
-    for (int it = tt; it < NSEG * CONV_BM; it += 256) {
-      const int il = it / CONV_BM, cl = it % CONV_BM, co = tc * CONV_BM + cl;
+    for (int it = tt; it < NSEG * CB; it += 256) {  // [image of the tile][CB couts]
+      const int il = it / CB, cl = it % CB, co = tc * CB + cl;
       const int img = min(Cf::ROWS ? (tp * 128) / HW : tp * NSEG + il, nimg - 1);
       float v = a.bias[co];
       if (a.temb) v += a.temb[trow + (long long)img * a.temb_img_stride + co];
@@ -3416,7 +3424,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r0 = 4 * (8 * hw + i), r = r0 + (lane >> 4), u = (lane & 15) ^ (r & 15), p = tp * 128 + r;
-      const T* src = p < a.M ? (const T*)a.resid + (size_t)p * a.Cout + tc * CONV_BM + u * 8 : (const T*)zero_of_block<T>(a);
+      // (64-cout items: units 8..15 of a row are not the tile's: the zero page)
+      const T* src = p < a.M && u * 8 < CB ? (const T*)a.resid + (size_t)p * a.Cout + tc * CB + u * 8
+                                           : (const T*)zero_of_block<T>(a);
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(rres + (k & 1) * RTILE + r0 * 256), 16, 0, 0);
     }
   };
@@ -3728,13 +3738,22 @@ bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 |
 static bool p5_dist(int tiles, int st) {
   return g_p5_dist && st > 2 && st <= 16 && (long long)tiles * st <= g_num_cus && (long long)tiles * 4 * 32 <= kTicketCap;
 }
-// its cost in chunk-times: the last-arriving slice reads all S partials serially (~0.3 a slice); shared, one slab
-// round trip a slice and the epilogue spread over the slices
-static double p5_combine_cost(int tiles, int st) { return st <= 1 ? 0.0 : p5_dist(tiles, st) ? 0.6 : 0.3 * st; }
+// its cost in chunk-times (a 64-channel chunk ~4.1 us at N <= 64), fitted to the per-op sweep of forced slice counts
+// (tools/p5_split_sweep.py, profiles/r06/p5_split_n*_r06f.txt): every split pays the partial's write-through and
+// drain, the arrival and the slab reads before its epilogue -- shared, ~2.5 (one poll, two overlapped slab round
+// trips); the last arriver ~2 + 0.5 a slice (its serial slice reads). (Round 5's 0.3 a slice over-split: the 16x16
+// level at N = 32 ran 2 slices at 25 us a launch where 1 takes 18.)
+static double p5_combine_cost(int tiles, int st, int cb) {
+  return st <= 1 ? 0.0 : cb == 128 && p5_dist(tiles, st) ? 2.5 : 2.0 + 0.5 * st;
+}
+// 64-cout items (CB = 64, W <= 8): a chunk's MFMA work halves, its staging does not -- ITSD_P5_C64_CHUNK chunk-times
+#ifndef ITSD_P5_C64_CHUNK
+#define ITSD_P5_C64_CHUNK 0.6
+#endif
 
-// K slices of a p5 launch: the S minimising ceil(items / CUs) x (chunks per slice + ~1.5 chunks of
-// prologue / epilogue) + the combine, bounded by the slab and ticket capacities
-static int p5_split(const ConvArgs& a, int tiles, int nch) {
+// K slices of a p5 launch at cout tile cb: the S minimising ceil(items / CUs) x (chunks per slice x chunk cost + ~1.5
+// chunks of prologue / epilogue) + the combine, bounded by the slab and ticket capacities
+static int p5_split(const ConvArgs& a, int tiles, int nch, int cb, double fc) {
   int S = 1;
   if (g_p5_split > 0) {
     S = std::min(g_p5_split, nch);
@@ -3742,11 +3761,11 @@ static int p5_split(const ConvArgs& a, int tiles, int nch) {
     double best = 1e30;
     for (int s = 1; s <= std::min(nch, 16); ++s) {
       const double waves = std::ceil((double)tiles * s / g_num_cus);
-      const double cost = waves * (std::ceil((double)nch / s) + 1.5) + p5_combine_cost(tiles, s);
+      const double cost = waves * (std::ceil((double)nch / s) * fc + 1.5) + p5_combine_cost(tiles, s, cb);
       if (cost < best - 1e-9) { best = cost; S = s; }
     }
   }
-  while (S > 1 && ((long long)tiles * S * 4 * 4096 > a.splitk_cap || (long long)tiles * 4 > kTicketCap)) --S;
+  while (S > 1 && ((long long)tiles * S * 128 * cb > a.splitk_cap || (long long)tiles * 4 > kTicketCap)) --S;
   return S;
 }
 
@@ -3810,56 +3829,81 @@ bool conv_p5_selected(const ConvArgs& a) {
 // 10-20 us launch with its gap; 3 left the 32x32 shortcuts at N = 32, the 8x8 ones at N = 64 and the 4x4 ones at N = 256
 // unfolded, 0.5-1.1 % slower steps, profiles/r05/p5_sc_launch_cost_r05aq.txt), or always with g_p5_sc = 2. Returns S2
 // (0: not folded) and the S to run with.
-static int p5_plan(const ConvArgs& a, int* S_out) {
+struct P5Plan {
+  int cb = 128, s = 1, s2 = 0;  // cout tile, 3x3 K slices, folded-shortcut K slices (0: not folded)
+  double cost = 0.0;
+};
+// 64-cout p5 items at W <= 8: 0 off (shipped), 1 auto (cost model), 2 always ("p5_c64", diagnostic builds). Measured and
+// dropped in round 6: bit-identical to 128-cout items, per-op steady state -8 % at N = 256's 4x4 level, but the
+// graph-replayed step equal at N = 256 (4.005 vs 4.001 ms) and 4-7 % slower at N = 64 / 32 (twice the items' prologues
+// and staging), profiles/r06/stepab_p5_c64_n*_r06h.txt, p5c64_*_r06h.txt
+int g_p5_c64 = 0;
+// Also the cout tile: 128, or 64 at W <= 8 (option p5_c64) where twice the tiles without a split cost less.
+static P5Plan p5_plan(const ConvArgs& a) {
   const int HW = a.Hout * a.Wout, nimg = a.M / HW;
   const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
-  const int tiles = ptiles * (a.Cout / CONV_BM), nch = (a.C1 + a.C2) / 64, nchx = (a.sc_C1 + a.sc_C2) / 64;
+  const int nch = (a.C1 + a.C2) / 64, nchx = (a.sc_C1 + a.sc_C2) / 64;
   const bool ws = a.splitk_ws && a.tickets;
-  const int S0 = ws ? p5_split(a, tiles, nch) : 1;
-  *S_out = S0;
-  if (!ws || !g_p5_sc || !a.sc_wfrag || nchx == 0 || a.sc_C1 % 64 || a.sc_C2 % 64 || (long long)tiles * 4 > kTicketCap)
-    return 0;
-  auto cost = [&](int s, int s2) {
-    const double waves = std::ceil((double)tiles * (s + s2) / g_num_cus);
-    const double c3 = std::ceil((double)nch / s) + 1.5, c1 = s2 ? 0.4 * std::ceil((double)nchx / s2) + 1.5 : 0.0;
-    return waves * std::max(c3, c1) + p5_combine_cost(tiles, s + s2);
-  };
-  double best = 1e30;
-  int bs = 0, bs2 = 0;
-  const int slo = g_p5_split > 0 ? S0 : 1, shi = g_p5_split > 0 ? S0 : std::min(nch, 16);
-  for (int s = slo; s <= shi; ++s)
-    for (int s2 = 1; s2 <= std::min(nchx, 16); ++s2) {
-      if ((long long)tiles * (s + s2) * 4 * 4096 > a.splitk_cap) break;
-      const double c = cost(s, s2);
-      if (c < best - 1e-9) { best = c; bs = s; bs2 = s2; }
+  const bool sc = ws && g_p5_sc && a.sc_wfrag && nchx > 0 && a.sc_C1 % 64 == 0 && a.sc_C2 % 64 == 0;
+  P5Plan best;
+  best.cost = 1e30;
+  for (int cb : {128, 64}) {
+    if (cb == 64 && (!g_p5_c64 || a.Wout > 8 || a.Cout % 64)) continue;
+    if (cb == 128 && g_p5_c64 == 2 && a.Wout <= 8 && a.Cout % 64 == 0) continue;
+    const int tiles = ptiles * (a.Cout / cb);
+    const double fc = cb == 128 ? 1.0 : ITSD_P5_C64_CHUNK;
+    auto cost = [&](int s, int s2) {
+      const double waves = std::ceil((double)tiles * (s + s2) / g_num_cus);
+      const double c3 = std::ceil((double)nch / s) * fc + 1.5, c1 = s2 ? 0.4 * std::ceil((double)nchx / s2) + 1.5 : 0.0;
+      return waves * std::max(c3, c1) + p5_combine_cost(tiles, s + s2, cb);
+    };
+    P5Plan p;
+    p.cb = cb;
+    p.s = ws ? p5_split(a, tiles, nch, cb, fc) : 1;
+    p.cost = cost(p.s, 0) + (sc ? ITSD_P5_SC_LAUNCH : 0.0);  // (unfolded: the shortcut's own launch besides)
+    if (sc && (long long)tiles * 4 <= kTicketCap) {
+      double bf = 1e30;
+      int bs = 0, bs2 = 0;
+      const int slo = g_p5_split > 0 ? p.s : 1, shi = g_p5_split > 0 ? p.s : std::min(nch, 16);
+      for (int s1 = slo; s1 <= shi; ++s1)
+        for (int s2 = 1; s2 <= std::min(nchx, 16); ++s2) {
+          if ((long long)tiles * (s1 + s2) * 128 * cb > a.splitk_cap) break;
+          const double c = cost(s1, s2);
+          if (c < bf - 1e-9) { bf = c; bs = s1; bs2 = s2; }
+        }
+      if (bs2 && (g_p5_sc == 2 || bf < p.cost)) {
+        p.s = bs;
+        p.s2 = bs2;
+        p.cost = bf;
+      }
     }
-  if (!bs2 || (g_p5_sc != 2 && best >= cost(S0, 0) + ITSD_P5_SC_LAUNCH)) return 0;
-  *S_out = bs;
-  return bs2;
+    if (p.cost < best.cost - 1e-9) best = p;
+  }
+  return best;
 }
 
 // launch_conv's shortcut fold for a p5 conv carrying sc_* candidates: folded?
-bool conv_p5_sc_fold(const ConvArgs& a) {
-  int S;
-  return conv_p5_selected(a) && p5_plan(a, &S) > 0;
-}
+bool conv_p5_sc_fold(const ConvArgs& a) { return conv_p5_selected(a) && p5_plan(a).s2 > 0; }
 
 static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   ConvArgs a = a0;
   const int HW = a.Hout * a.Wout, nimg = a.M / HW;
   const int ptiles = HW > 128 ? a.M / 128 : (nimg + 128 / HW - 1) / (128 / HW);
-  const int tiles = ptiles * (a.Cout / CONV_BM);
-  int S = 1;
-  const int S2 = p5_plan(a, &S);
-  if (a.sc_C1 + a.sc_C2 && !S2) return hipErrorInvalidValue;  // (the caller folds only what p5_plan accepts)
-  a.ksplit = S;
-  a.sc_split = S2;
-  const int items = tiles * (S + S2);
-  a.kdist = g_p5_dist == 1 && p5_dist(tiles, S + S2);
+  const P5Plan p = p5_plan(a);
+  if (a.sc_C1 + a.sc_C2 && !p.s2) return hipErrorInvalidValue;  // (the caller folds only what p5_plan accepts)
+  const int tiles = ptiles * (a.Cout / p.cb);
+  a.ksplit = p.s;
+  a.sc_split = p.s2;
+  const int items = tiles * (p.s + p.s2);
+  a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2);
   const dim3 g(std::min(items, g_num_cus));
   if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p5_kernel<64>, g, dim3(512), 0, s, a);
   else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);
   else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p5_kernel<16>, g, dim3(512), 0, s, a);
+#ifdef ITSD_DIAG
+  else if (a.Wout == 8 && p.cb == 64) ITSD_LAUNCH((conv3x3_gn_p5_kernel<8, 64>), g, dim3(512), 0, s, a);
+  else if (p.cb == 64) ITSD_LAUNCH((conv3x3_gn_p5_kernel<4, 64>), g, dim3(512), 0, s, a);
+#endif
   else if (a.Wout == 8) ITSD_LAUNCH(conv3x3_gn_p5_kernel<8>, g, dim3(512), 0, s, a);
   else ITSD_LAUNCH(conv3x3_gn_p5_kernel<4>, g, dim3(512), 0, s, a);
   return hipGetLastError();

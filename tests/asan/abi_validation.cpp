@@ -74,6 +74,7 @@ int main() {
   expect("set_option small_minks=2 (diagnostic)", itsd_set_option("small_minks", 2), ITSD_ERR_INVALID);
   expect("set_option splitk=2 (diagnostic)", itsd_set_option("splitk", 2), ITSD_ERR_INVALID);
   expect("set_option conv1x1=2 (diagnostic)", itsd_set_option("conv1x1", 2), ITSD_ERR_INVALID);
+  expect("set_option p5_c64=2 (diagnostic)", itsd_set_option("p5_c64", 2), ITSD_ERR_INVALID);
   expect("set_option p5_dist=3", itsd_set_option("p5_dist", 3), ITSD_ERR_INVALID);
   expect("set_option p5_dist=1", itsd_set_option("p5_dist", 1), ITSD_OK);
   expect("set_option conv_variant=3 (removed)", itsd_set_option("conv_variant", 3), ITSD_ERR_INVALID);

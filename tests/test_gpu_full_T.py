@@ -1,32 +1,31 @@
-"""Full-length sampled images and scores against the oracle ("Pin full-length sampled
-images and scores"; north_star: "sampled images match the reference PyTorch CPU path on fixed seeds
-within a stated fp32 tolerance").
+"""Full-length sampled images and scores against the REFERENCE's own fp32 trajectories (north_star: "sampled
+images match the reference PyTorch CPU path on fixed seeds within a stated fp32 tolerance").
 
-One module fixture runs, on the GPU:
-  C1   Main.py's eval (config/config.yaml keys through itsd.entry, ``Diffusion/Train.py:808-843``):
-       Arch A, T = 1000, fp32 (the reference's precision), synthetic weights, batch_size 1 and 2 --
-       the whole ancestral loop ``Diffusion/Diffusion.py:84-102`` in Philox mode;
-  C2   one bf16 random-search round of N = 256 Philox candidates at T = 1000 (the bench's round,
-       ``search/search_algorithm.py:54-83``) scored by the OracleVerifier (``search/verifier.py:45-66``),
-and then the oracle's full 1000-step loop (``oracle.ref_cpu.p_sample_loop``, fp32 CPU) over the two
-C1 runs' 3 images and 3 of the 256 candidates (indices 0, 129, 255) in ONE batched loop, each image
-fed its own counter-based noise (``R.philox_normal``: the seed the run used, the image's global
-element offset), so every comparison is one image's whole trajectory.
+Fixtures (tests/golden/full_C*.npz, tools/gen_golden_full.py, build container): the reference samplers
+(``Diffusion/Diffusion.py:50-102``, ``DiffusionFreeGuidence/DiffusionCondition.py:55-105``) imported from
+/root/reference and their ``p_mean_variance`` driven over the WHOLE schedule with the throughput mode's Philox noise
+(the same per-step z the GPU draws), their x0 and the reference OracleVerifier's scores, for candidates of the bench
+shards' rounds; the GPU runs each shard's whole round through ``SearchEngine`` (bf16, graph-replayed):
+  C2   a random-search round of N = 256, Arch A 32 px, T = 1000: candidates 0 / 129 / 255;
+  C3   a zero-order round of the C3 shard N_local = 32 (Arch C CFG, w = 1.8, betas 1e-4 .. 0.028, label 3, pivot +
+       0.05 z): the 2N = 64 guided batch, candidates 0 / 31;
+  C4   a random round of the C4 shard N_local = 16 (Arch A 64 px): candidates 0 / 15;
+  C5   a path-search round of the C5 shard N = 128 at T = 3000 (fine_tune_extended_T.py schedule, pivot + 0.1 z):
+       candidates 0 / 64 / 127.
+C1 (``Main.py``'s eval through itsd.entry, fp32) draws x_T from torch's CUDA generator, which cannot be replayed on
+the host: its three images run the oracle's loop (``oracle.ref_cpu.p_sample_loop``) here on the box.
 
-Tolerances: DERIVED, not tuned (VERDICT r4 #5c; tools/derive_tolerances.py -> tests/golden/tolerance_derivation.json,
-DESIGN.md section 4). Two drifts of the oracle's own whole loop on CPU:
-  fp32   the fp32 oracle against the same loop in fp64 (weights, activations, x): the GPU fp32 path and the
-         oracle are two fp32 evaluations of one fp64 trajectory, so |GPU - oracle| <= 2 x drift; bound =
-         4 x 2 x drift (x2 margin).   C1 Arch A T=1000: drift 6.5e-5 on the saved image -> 5.2e-4;
-         C1c tiny CFG w=1.8 T=1000: drift 4.5e-4 -> 3.6e-3.
-  bf16   a bf16 emulation of the oracle (weights bf16; every conv's input and output rounded to bf16 with
-         fp32 accumulation, as the GPU's bf16 path) against the fp32 oracle: the GPU bf16 path and the
-         emulation are two bf16 evaluations of one fp32 trajectory; bound = 2 x the emulation's drift.
-         C2 T=1000: x0 rel-L2 3.0e-2 -> 6.1e-2; C5 T=3000: see the JSON (the T=3000 images of the synthetic
-         model saturate to +-1, so their rel-L2 counts sign flips: 2 sqrt(k / 3072)).
+Tolerances: DERIVED, not tuned (tools/derive_tolerances.py -> tests/golden/tolerance_derivation.json, DESIGN.md
+section 4):
+  fp32   4 x 2 x the oracle's own fp32-vs-fp64 drift over the loop (C1: 5.2e-4 on the saved image; C1c tiny CFG
+         w = 1.8: 3.6e-3);
+  bf16   2 x the drift of a bf16 emulation of the loop (bf16 weights, every conv's input and output rounded to bf16
+         with fp32 accumulation, as the GPU's bf16 path) against the fp32 trajectory -- C2 / C5 against the oracle,
+         C3 / C4 against the reference fixtures themselves (the T = 3000 images of the synthetic model saturate to
+         +-1, so C5's rel-L2 counts sign flips);
   scores an exact consequence of the image (_check_score): the search's score equals the verifier on the
-         candidate's own x0 (1e-6), and differs from the oracle trajectory's score by at most what the measured
-         x0 difference implies (Cauchy-Schwarz on the variance; no sampled bound).
+         candidate's own x0 (1e-6), and differs from the reference's score by at most what the measured x0
+         difference implies (Cauchy-Schwarz on the variance; no sampled bound).
 Measured values are printed.
 """
 import dataclasses
@@ -37,11 +36,12 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import golden
 from oracle import ref_cpu as R
 from itsd import entry as E
-from itsd.arch import ARCH_A, ARCH_TINY_CFG
-from itsd.diffusion import GaussianDiffusionSampler
-from itsd.model import UNet
+from itsd.arch import ARCH_A, ARCH_C, ARCH_TINY_CFG
+from itsd.diffusion import CondGaussianDiffusionSampler, GaussianDiffusionSampler
+from itsd.model import CondUNet, UNet
 from itsd.search import SearchEngine
 from itsd.verifier import OracleVerifier
 from itsd.weights import synthetic_state_dict
@@ -56,19 +56,24 @@ FULL_T_BF16_SCORE = _TOL["FULL_T_BF16_SCORE"]
 FULL_T_FP32_CFG_MAXABS = _TOL["FULL_T_FP32_CFG_MAXABS"]  # 4 x 2 x the guided loop's fp32-vs-fp64 drift (C1c)
 C5_BF16_REL_L2 = _TOL["C5_BF16_REL_L2"]                  # 2 x the bf16 emulation's drift at T = 3000
 C5_BF16_SCORE = _TOL["C5_BF16_SCORE"]
+C3_BF16_REL_L2 = _TOL["C3_BF16_REL_L2"]                  # 2 x the bf16 emulation's drift vs the reference (C3)
+C3_BF16_SCORE = _TOL["C3_BF16_SCORE"]
+C4_BF16_REL_L2 = _TOL["C4_BF16_REL_L2"]                  # 2 x the bf16 emulation's drift vs the reference (C4)
+C4_BF16_SCORE = _TOL["C4_BF16_SCORE"]
+FULL_T_BF16_RAW_REL_L2 = _TOL["FULL_T_BF16_RAW_REL_L2"]  # the same drifts on x0 before the final clip
+C3_BF16_RAW_REL_L2 = _TOL["C3_BF16_RAW_REL_L2"]
+C4_BF16_RAW_REL_L2 = _TOL["C4_BF16_RAW_REL_L2"]
+C5_BF16_RAW_REL_L2 = _TOL["C5_BF16_RAW_REL_L2"]
 
 T = 1000
 PER = 3 * 32 * 32
-STREAM_XT = 0xF0000000  # itsd.search._STREAM_XT: candidate x_T of round 0
-CANDS = (0, 129, 255)
-ENGINE_SEED = 21
 
 
 def _rel_l2(a, b):
     return (torch.linalg.norm((a - b).flatten()) / torch.linalg.norm(b.flatten())).item()
 
 
-def _check_score(tag, got_x0, got_score, ref_x0, sampled_bound):
+def _check_score(tag, got_x0, got_score, ref_x0, sampled_bound, ref_score=None):
     """The OracleVerifier score of a candidate, in two exact steps (no sampled bound):
     (1) the search's score IS the verifier on the candidate's own image: |score - R.oracle_score(x0)| <= 1e-6;
     (2) against the oracle trajectory's score, the difference the image difference implies: with d = x0 - ref,
@@ -83,7 +88,9 @@ def _check_score(tag, got_x0, got_score, ref_x0, sampled_bound):
     assert abs(float(got_score) - self_score) <= 1e-6, (tag, float(got_score), self_score)
     v1, v2 = torch.var(r).item(), torch.var(g).item()
     implied = (2 * torch.std(r).item() * torch.std(d).item() + torch.var(d).item()) / ((1 + v1) * (1 + v2))
-    s_ref = R.oracle_score(ref_x0.unsqueeze(0))
+    s_ref = R.oracle_score(ref_x0.unsqueeze(0)) if ref_score is None else float(ref_score)
+    if ref_score is not None:  # the reference verifier's own score of its x0 (fixture) is the oracle's formula
+        assert abs(s_ref - R.oracle_score(ref_x0.unsqueeze(0))) <= 1e-6, (tag, s_ref)
     ds = abs(float(got_score) - s_ref)
     print(f"{tag}: score {float(got_score):.6f} (verifier on its own x0 {self_score:.6f}) vs oracle {s_ref:.6f}: "
           f"|d| {ds:.2e}, implied by the x0 difference <= {implied:.2e} (sampled emulation figure {sampled_bound:.2e})")
@@ -104,26 +111,13 @@ def full_T(tmp_path_factory):
         c1.append({"x_T": res["noisy"].cpu(), "sampled": res["sampled"].cpu(), "seed": int(res["sampler_seed"])})
         torch.cuda.empty_cache()
     out["c1"] = c1
-    # ---- C2: a bf16 N = 256 Philox round (the bench's round protocol)
+    # ---- the oracle: one batched fp32 loop over C1's 3 images, each with its own noise stream
     a = ARCH_A
-    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
-    net.load_state_dict(synthetic_state_dict(a, 0))
-    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, T)
-    eng = SearchEngine(smp, OracleVerifier(), seed=ENGINE_SEED)
-    r = eng.run_round(0, 256, (1, 3, 32, 32))
-    run_seed = (ENGINE_SEED * 1000003 + 0) & ((1 << 62) - 1)  # SearchEngine.run_round's sampler key
-    out["c2"] = {"x0": r.local_images.cpu(), "scores": r.scores.clone(), "run_seed": run_seed}
-    del eng, smp, net
-    torch.cuda.empty_cache()
-    # ---- the oracle: one batched fp32 loop over the 6 images, each with its own noise stream
     x_T, streams = [], []  # streams[i] = (seed, first global element of image i)
     for run in c1:
         for j in range(run["x_T"].shape[0]):
             x_T.append(run["x_T"][j])
             streams.append((run["seed"], j * PER))
-    for i in CANDS:
-        x_T.append(R.philox_normal(ENGINE_SEED, STREAM_XT, np.arange(i * PER, (i + 1) * PER)).reshape(3, 32, 32))
-        streams.append((run_seed, i * PER))
     x_T = torch.stack(x_T)
 
     def noise(step, xx):
@@ -135,6 +129,49 @@ def full_T(tmp_path_factory):
         out["oracle_x0"] = R.p_sample_loop(fw, x_T, R.schedule(1e-4, 0.02, T), noise)
     out["oracle_x_T"] = x_T
     return out
+
+
+def _round(fx, net, smp, shape, kind, labels=None):
+    """The fixture's round on the GPU through SearchEngine (the bench shard's protocol): its candidates' x_T must be
+    the fixture's (the engine's Philox x_T; pivot + scale z with one fp32 rounding), then the whole sampler run."""
+    eng = SearchEngine(smp, OracleVerifier(), seed=int(fx["seed"]))
+    rnd, n = int(fx["round"]), int(fx["n"])
+    pivot, scale = None, 1.0
+    if kind != "random":
+        pivot, scale = eng.initial_noise(shape), float(fx["scale"])
+        assert torch.equal(pivot.cpu(), torch.from_numpy(fx["pivot"]).reshape(shape))
+    cands = [int(c) for c in fx["cands"]]
+    xT = torch.cat([eng.candidate_noise(rnd, i, 1, shape, pivot=pivot, scale=scale) for i in cands]).cpu()
+    dx = (xT - torch.from_numpy(fx["x_T"])).abs().max().item()
+    assert dx <= 1e-6, dx  # (the fused multiply-add's one rounding, emulated in fp64 on the host)
+    r = eng.run_round(rnd, n, shape, pivot=pivot, scale=scale, labels=labels, kind=kind)
+    # the same shard once more without the final clip (the synthetic model's images saturate to +-1: the pre-clip x0
+    # is the continuous comparison): every candidate's trajectory is a function of (seed, global index) alone
+    x = eng.candidate_noise(rnd, 0, n, shape, pivot=pivot, scale=scale)
+    lab = labels.to(x.device).flatten().repeat(n) if labels is not None else None
+    smp.run(x, labels=lab, seed=(int(fx["seed"]) * 1000003 + rnd) & ((1 << 62) - 1), noise_offset=0, clip=False)
+    raw = x.cpu()
+    assert torch.equal(raw.clamp(-1, 1), r.local_images.cpu())  # (the round's images are this run's, clipped)
+    return cands, r.local_images.cpu(), r.scores.clone(), raw
+
+
+def _check_raw(tag, fx, cands, raw, raw_bound):
+    ref = torch.from_numpy(fx["x0_raw"])
+    for k, i in enumerate(cands):
+        rel = _rel_l2(raw[i], ref[k])
+        print(f"{tag} bf16 candidate {i}: pre-clip x0 rel-L2 vs the reference {rel:.3e} (bound {raw_bound:.3e}; "
+              f"reference |x0| max {ref[k].abs().max().item():.1f})")
+        assert rel <= raw_bound
+
+
+def _check_round(tag, fx, cands, x0, scores, rel_bound, score_bound):
+    ref = torch.from_numpy(fx["x0"])
+    for k, i in enumerate(cands):
+        rel = _rel_l2(x0[i], ref[k])
+        print(f"{tag} bf16 candidate {i}: T={int(fx['T'])} x0 rel-L2 vs the reference {rel:.3e} (bound {rel_bound:.3e}), "
+              f"max|d| {(x0[i] - ref[k]).abs().max().item():.3e}")
+        assert rel <= rel_bound
+        _check_score(f"{tag} candidate {i}", x0[i], scores[i], ref[k], score_bound, ref_score=fx["scores"][k])
 
 
 def test_C1_main_eval_T1000_fp32_vs_oracle(full_T):
@@ -151,60 +188,62 @@ def test_C1_main_eval_T1000_fp32_vs_oracle(full_T):
         k += n
 
 
-def test_C2_bf16_round_T1000_candidates_and_scores_vs_oracle(full_T):
-    """Three candidates of one bf16 N = 256 round: the denoised x0 (rel-L2) and the OracleVerifier
-    score the search prunes on, against the fp32 oracle's full loop and R.oracle_score."""
-    c2 = full_T["c2"]
-    for k, i in enumerate(CANDS):
-        # the round's x_T is the Philox generator's (itsd_noise == R.philox_normal is pinned by
-        # test_gpu_search.test_philox_noise_kernel_matches_oracle), so the oracle started from it
-        ref = full_T["oracle_x0"][3 + k]
-        got = c2["x0"][i]
-        rel = _rel_l2(got, ref)
-        print(f"C2 bf16 candidate {i}: x0 rel-L2 {rel:.3e}, max|d| {(got - ref).abs().max().item():.3e}")
-        assert rel <= FULL_T_BF16_REL_L2
-        _check_score(f"C2 candidate {i}", got, c2["scores"][i], ref, FULL_T_BF16_SCORE)
-
-
-C5_T, C5_N, C5_CANDS, C5_SEED = 3000, 128, (0, 64, 127), 33
-STREAM_PERTURB = 0xE0000000  # itsd.search._STREAM_PERTURB: perturbed candidates (pivot + scale z) of round 0
-
-
-def test_C5_path_search_round_T3000_candidates_and_scores_vs_oracle():
-    """C5 at full length (VERDICT r4 #5a): one bf16 path-search round (``search/search_algorithm.py:265-336``;
-    candidates = pivot + 0.1 z) of the bench shard N = 128 over the whole T = 3000 schedule of
-    ``fine_tune_extended_T.py`` (betas 1e-4 .. 0.02), three candidates (0, 64, 127) -- the denoised x0 and the
-    OracleVerifier score the search prunes on -- against the oracle's full 3000-step fp32 loop on the same
-    x_T and Philox noise. Bounds: C5_BF16_REL_L2 / C5_BF16_SCORE, derived (tests/golden/tolerance_derivation.json)."""
-    a = dataclasses.replace(ARCH_A, T=C5_T)
+def test_C2_bf16_round_T1000_candidates_and_scores_vs_reference():
+    """Three candidates of one bf16 N = 256 random-search round (the bench's round): the denoised x0 (rel-L2) and the
+    OracleVerifier score the search prunes on, against the reference's own fp32 loop (full_C2.npz)."""
+    fx = golden("full_C2")
+    a = ARCH_A
     net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
     net.load_state_dict(synthetic_state_dict(a, 0))
-    smp = GaussianDiffusionSampler(net, 1e-4, 0.02, C5_T)
-    eng = SearchEngine(smp, OracleVerifier(), seed=C5_SEED)
-    shape = (1, 3, 32, 32)
-    pivot = eng.initial_noise(shape)
-    r = eng.run_round(0, C5_N, shape, pivot=pivot, scale=0.1, kind="path")
-    run_seed = (C5_SEED * 1000003 + 0) & ((1 << 62) - 1)
-    # the candidates' x_T regenerated on the device (the same kernel, bit-identical) -> the oracle's start
-    x_T = torch.cat([eng.candidate_noise(0, i, 1, shape, pivot=pivot, scale=0.1) for i in C5_CANDS]).cpu()
-    x0 = r.local_images.cpu()
-    scores = r.scores.clone()
-    del eng, smp, net
-    torch.cuda.empty_cache()
-    streams = [(run_seed, i * PER) for i in C5_CANDS]
+    smp = GaussianDiffusionSampler(net, 1e-4, float(fx["beta_T"]), int(fx["T"]))
+    cands, x0, scores, raw = _round(fx, net, smp, (1, 3, 32, 32), "random")
+    _check_round("C2", fx, cands, x0, scores, FULL_T_BF16_REL_L2, FULL_T_BF16_SCORE)
+    _check_raw("C2", fx, cands, raw, FULL_T_BF16_RAW_REL_L2)
 
-    def noise(step, xx):
-        return torch.stack([R.philox_normal(sd_, step, np.arange(o, o + PER)).reshape(3, 32, 32) for sd_, o in streams])
 
-    sd = synthetic_state_dict(a, 0)
-    fw = lambda xx, tt: R.unet_forward(sd, xx, tt, a.ch, a.ch_mult, a.attn, a.num_res_blocks)
-    with torch.no_grad():
-        ref = R.p_sample_loop(fw, x_T, R.schedule(1e-4, 0.02, C5_T), noise)
-    for k, i in enumerate(C5_CANDS):
-        rel = _rel_l2(x0[i], ref[k])
-        print(f"C5 bf16 path candidate {i}: T=3000 x0 rel-L2 {rel:.3e}, max|d| {(x0[i] - ref[k]).abs().max().item():.3e}")
-        assert rel <= C5_BF16_REL_L2
-        _check_score(f"C5 candidate {i}", x0[i], scores[i], ref[k], C5_BF16_SCORE)
+def test_C3_cfg_zero_order_round_T1000_candidates_and_scores_vs_reference():
+    """C3 at full length: one bf16 zero-order round of the C3 shard (Arch C, ``MainCondition.py``;
+    N_local = 32 neighbours pivot + 0.05 z, label 3 -> the 2N = 64 guided batch, w = 1.8, T = 1000) through
+    SearchEngine, two candidates' x0 and OracleVerifier scores (what ``ZeroOrderSearch`` prunes on,
+    ``search_algorithm.py:180-196``) against the reference's own guided loop (full_C3.npz)."""
+    fx = golden("full_C3")
+    c = ARCH_C
+    net = CondUNet(c.T, c.num_labels, c.ch, c.ch_mult, c.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
+    net.load_state_dict(synthetic_state_dict(c, 0))
+    smp = CondGaussianDiffusionSampler(net, 1e-4, float(fx["beta_T"]), int(fx["T"]), w=float(fx["w"]))
+    labels = torch.tensor([int(fx["label"])], dtype=torch.int32)
+    cands, x0, scores, raw = _round(fx, net, smp, (1, 3, 32, 32), "zero_order", labels=labels)
+    _check_round("C3", fx, cands, x0, scores, C3_BF16_REL_L2, C3_BF16_SCORE)
+    _check_raw("C3", fx, cands, raw, C3_BF16_RAW_REL_L2)
+
+
+def test_C4_64px_round_T1000_candidates_and_scores_vs_reference():
+    """C4 at full length: one bf16 random round of the C4 shard (Arch A at 64 px, N_local = 16,
+    T = 1000) through SearchEngine, two candidates' x0 and scores against the reference's own loop (full_C4.npz)."""
+    fx = golden("full_C4")
+    a = dataclasses.replace(ARCH_A, img_size=64)
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=64, precision="bf16").to("cuda:0")
+    net.load_state_dict(synthetic_state_dict(a, 0))
+    smp = GaussianDiffusionSampler(net, 1e-4, float(fx["beta_T"]), int(fx["T"]))
+    cands, x0, scores, raw = _round(fx, net, smp, (1, 3, 64, 64), "random")
+    _check_round("C4", fx, cands, x0, scores, C4_BF16_REL_L2, C4_BF16_SCORE)
+    _check_raw("C4", fx, cands, raw, C4_BF16_RAW_REL_L2)
+
+
+def test_C5_path_search_round_T3000_candidates_and_scores_vs_reference():
+    """C5 at full length: one bf16 path-search round (``search/search_algorithm.py:265-336``; candidates = pivot +
+    0.1 z) of the bench shard N = 128 over the whole T = 3000 schedule of ``fine_tune_extended_T.py`` (betas 1e-4 ..
+    0.02), three candidates -- the denoised x0 and the OracleVerifier score the search prunes on -- against the
+    reference's own 3000-step loop on the same x_T and Philox noise (full_C5.npz). Bounds: C5_BF16_REL_L2 /
+    C5_BF16_SCORE, derived (tests/golden/tolerance_derivation.json)."""
+    fx = golden("full_C5")
+    a = dataclasses.replace(ARCH_A, T=int(fx["T"]))
+    net = UNet(a.T, a.ch, a.ch_mult, a.attn, a.num_res_blocks, 0.0, img_size=32, precision="bf16").to("cuda:0")
+    net.load_state_dict(synthetic_state_dict(a, 0))
+    smp = GaussianDiffusionSampler(net, 1e-4, float(fx["beta_T"]), int(fx["T"]))
+    cands, x0, scores, raw = _round(fx, net, smp, (1, 3, 32, 32), "path")
+    _check_round("C5", fx, cands, x0, scores, C5_BF16_REL_L2, C5_BF16_SCORE)
+    _check_raw("C5", fx, cands, raw, C5_BF16_RAW_REL_L2)
 
 
 def test_C1c_main_condition_eval_T1000_fp32_vs_oracle(tmp_path):

@@ -21,7 +21,7 @@ from itsd.weights import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 REL_L2_BF16 = 2e-2
-_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1}
+_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1, "p5_sc": 1}
 
 
 def _rel_l2(a, b):

@@ -108,7 +108,7 @@ def test_conv_tile_options():
         rt.set_option("spin_bound", -1)
     # (round 6) measurement switches are diagnostic-build only: the shipped ABI refuses them
     for key, val in (("conv_dbg", 1), ("conv_dbg", 0), ("attn_cs", 2), ("attn_aq", 32), ("p4_xcd", 1),
-                     ("small_minks", 2), ("splitk", 2), ("conv1x1", 2)):
+                     ("small_minks", 2), ("splitk", 2), ("conv1x1", 2), ("p5_c64", 2)):
         with pytest.raises(rt.ItsdError, match="diagnostic build"):
             rt.set_option(key, val)
     for key, val in (("splitk", 0), ("splitk", 1), ("conv1x1", 0), ("conv1x1", 1)):  # their shipped values stay

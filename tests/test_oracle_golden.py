@@ -192,3 +192,37 @@ def test_full_T_tolerances_follow_from_the_recorded_drifts():
     assert t["C5_BF16_SCORE"] == f16 * d["C5_bf16_emulation"]["score_absdiff_max"]
     assert 1e-2 < d["C2_bf16_emulation"]["x0_rel_l2_max"] < 5e-2
     assert d["C1_archA_fp32_vs_fp64"]["image_maxabs"] < 1e-4 < d["C2_bf16_emulation"]["x0_rel_l2_max"]
+    # (round 6) C2-C5 measured against the reference's own trajectories (tests/golden/full_C*.npz), on x0 and on x0
+    # before the final clip (the synthetic model's full-length images saturate to +-1)
+    for part, rel, score, raw in (("C2", "FULL_T_BF16_REL_L2", "FULL_T_BF16_SCORE", "FULL_T_BF16_RAW_REL_L2"),
+                                  ("C3", "C3_BF16_REL_L2", "C3_BF16_SCORE", "C3_BF16_RAW_REL_L2"),
+                                  ("C4", "C4_BF16_REL_L2", "C4_BF16_SCORE", "C4_BF16_RAW_REL_L2"),
+                                  ("C5", "C5_BF16_REL_L2", "C5_BF16_SCORE", "C5_BF16_RAW_REL_L2")):
+        e = d[f"{part}_bf16_emulation"]
+        assert e["against"] == f"tests/golden/full_{part}.npz (the reference's own fp32 loop)"
+        assert t[rel] == f16 * e["x0_rel_l2_max"] and t[score] == f16 * e["score_absdiff_max"]
+        assert t[raw] == f16 * e["raw_rel_l2_max"]
+
+
+def test_full_length_reference_fixtures():
+    """tests/golden/full_C*.npz (tools/gen_golden_full.py, the reference's samplers driven with the Philox noise): the
+    candidates' x_T are the engine's Philox draws (oracle.ref_cpu.philox_normal; pivot + scale z), x0 is the
+    clipped pre-clip x0, and the scores are the OracleVerifier formula of x0."""
+    import numpy as np
+    from oracle import ref_cpu as R
+    for part, per in (("C2", 3072), ("C3", 3072), ("C4", 3 * 64 * 64), ("C5", 3072)):
+        fx = golden(f"full_{part}")
+        seed, rnd, cands = int(fx["seed"]), int(fx["round"]), [int(c) for c in fx["cands"]]
+        shape = fx["x_T"].shape[1:]
+        for k, i in enumerate(cands[:1]):
+            if "pivot" in fx.files:
+                z = R.philox_normal(seed, 0xE0000000 + rnd, np.arange(i * per, (i + 1) * per)).reshape(shape)
+                want = (np.float64(fx["scale"]) * z.double().numpy() + fx["pivot"].astype(np.float64)).astype(np.float32)
+                piv = R.philox_normal(seed, 0xD0000000, np.arange(per)).reshape(shape).numpy()
+                assert np.array_equal(piv, fx["pivot"])
+            else:
+                want = R.philox_normal(seed, 0xF0000000 + rnd, np.arange(i * per, (i + 1) * per)).reshape(shape).numpy()
+            assert np.array_equal(want, fx["x_T"][k]), part
+        assert np.array_equal(np.clip(fx["x0_raw"], -1, 1), fx["x0"]), part
+        for k in range(len(cands)):
+            assert abs(float(fx["scores"][k]) - R.oracle_score(torch.from_numpy(fx["x0"][k:k + 1]))) <= 1e-6, part

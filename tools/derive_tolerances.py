@@ -136,15 +136,22 @@ def bf16_emulation_vs_fixture(name, a, beta_T, w=None):
     try:
         t0 = time.time()
         with torch.no_grad():
-            emu = R.p_sample_loop(fwb, x_T, R.schedule(1e-4, beta_T, T), noise).double()
+            raw = R.p_sample_loop(fwb, x_T, R.schedule(1e-4, beta_T, T), noise, clip=False).double()
         print(f"  {name} bf16-emulation loop {time.time() - t0:.0f}s", flush=True)
     finally:
         F.conv2d, F.conv_transpose2d = conv2d, convt
+    emu = raw.clamp(-1, 1)
+    ref_raw = torch.from_numpy(fx["x0_raw"]).double()
     rel = [((emu[i] - ref[i]).norm() / ref[i].norm()).item() for i in range(len(cands))]
+    rel_raw = [((raw[i] - ref_raw[i]).norm() / ref_raw[i].norm()).item() for i in range(len(cands))]
     dscore = [abs(R.oracle_score(emu[i:i + 1].float()) - float(fx["scores"][i])) for i in range(len(cands))]
-    print(f"  {name} bf16 emulation vs the reference: x0 rel-L2 {rel}, score |d| {dscore}", flush=True)
+    print(f"  {name} bf16 emulation vs the reference: x0 rel-L2 {rel}, pre-clip x0 rel-L2 {rel_raw}, score |d| {dscore}",
+          flush=True)
     return {"images": len(cands), "against": f"tests/golden/full_{name}.npz (the reference's own fp32 loop)",
-            "x0_rel_l2_max": max(rel), "x0_rel_l2_mean": float(np.mean(rel)), "score_absdiff_max": max(dscore)}
+            "x0_rel_l2_max": max(rel), "x0_rel_l2_mean": float(np.mean(rel)),
+            "raw_rel_l2_max": max(rel_raw), "raw_rel_l2_mean": float(np.mean(rel_raw)),
+            "raw_absmax": ref_raw.abs().max().item(), "saturated_frac": (ref.abs() >= 0.999).double().mean().item(),
+            "score_absdiff_max": max(dscore)}
 
 
 def main():
@@ -160,12 +167,17 @@ def main():
     res = {"factor_fp32": FACTOR_FP32, "factor_bf16": FACTOR_BF16, "T": T}
     parts = {"C1c": "C1c_cfg_fp32_vs_fp64", "C1": "C1_archA_fp32_vs_fp64", "C2": "C2_bf16_emulation",
              "C5": "C5_bf16_emulation", "C3": "C3_bf16_emulation", "C4": "C4_bf16_emulation"}
-    if args.only in ("C3", "C4"):  # (round 6) against the reference fixtures of tools/gen_golden_full.py
+    if args.only in ("C2", "C3", "C4", "C5"):  # (round 6) against the reference fixtures of tools/gen_golden_full.py
         if args.only == "C3":
             from itsd.arch import ARCH_C
             r = bf16_emulation_vs_fixture("C3", ARCH_C, 0.028, w=1.8)
-        else:
+        elif args.only == "C4":
             r = bf16_emulation_vs_fixture("C4", dataclasses.replace(ARCH_A, img_size=64), 0.02)
+        elif args.only == "C5":
+            r = bf16_emulation_vs_fixture("C5", dataclasses.replace(ARCH_A, T=3000), 0.02)
+            r["T"] = 3000
+        else:
+            r = bf16_emulation_vs_fixture("C2", ARCH_A, 0.02)
         with open(f"{args.out}.{args.only}.json", "w") as fh:
             json.dump(r, fh, indent=1)
         return
@@ -240,6 +252,10 @@ def _finish(res, args):
         "FULL_T_BF16_SCORE": FACTOR_BF16 * res["C2_bf16_emulation"]["score_absdiff_max"],
         "C5_BF16_REL_L2": FACTOR_BF16 * res["C5_bf16_emulation"]["x0_rel_l2_max"],
         "C5_BF16_SCORE": FACTOR_BF16 * res["C5_bf16_emulation"]["score_absdiff_max"],
+        "FULL_T_BF16_RAW_REL_L2": FACTOR_BF16 * res["C2_bf16_emulation"]["raw_rel_l2_max"],
+        "C5_BF16_RAW_REL_L2": FACTOR_BF16 * res["C5_bf16_emulation"]["raw_rel_l2_max"],
+        "C3_BF16_RAW_REL_L2": FACTOR_BF16 * res["C3_bf16_emulation"]["raw_rel_l2_max"],
+        "C4_BF16_RAW_REL_L2": FACTOR_BF16 * res["C4_bf16_emulation"]["raw_rel_l2_max"],
         "C3_BF16_REL_L2": FACTOR_BF16 * res["C3_bf16_emulation"]["x0_rel_l2_max"],
         "C3_BF16_SCORE": FACTOR_BF16 * res["C3_bf16_emulation"]["score_absdiff_max"],
         "C4_BF16_REL_L2": FACTOR_BF16 * res["C4_bf16_emulation"]["x0_rel_l2_max"],

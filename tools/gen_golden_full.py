@@ -6,7 +6,9 @@ The reference's own samplers (``Diffusion/Diffusion.py:50-102``, ``DiffusionFree
 (``oracle.ref_cpu.philox_normal``, bit-exact with the device generator: ``test_philox_noise_kernel_matches_oracle``),
 replicating the loop body of ``forward`` (``x_t = mean + sqrt(var) * noise``, no noise at t = 0, NaN assert,
 final clip). Each fixture holds only inputs and outputs -- the candidates' x_T, the denoised x0 and the
-reference OracleVerifier's score (``search/verifier.py:45-66``) -- for candidates of the bench's shard rounds:
+reference OracleVerifier's score (``search/verifier.py:45-66``), and x_0 before the final clip (the synthetic
+model's full-length images saturate to +-1, so the clipped x0 alone would compare sign flips) -- for candidates of
+the bench's shard rounds:
 
   full_C2  Arch A 32 px, T = 1000, a random-search round of N = 256 (engine seed 21), candidates 0 / 129 / 255
   full_C3  Arch C CFG (MainCondition.py), w = 1.8, betas 1e-4 .. 0.028, T = 1000, a zero-order round of the C3
@@ -85,7 +87,7 @@ def drive(sampler, x_T, run_seed, cands, per, T, labels=None):
             assert torch.isnan(x_t).int().sum() == 0, "nan in tensor."
             if time_step % 200 == 0:
                 print(f"    t={time_step} ({time.time() - t0:.0f}s)", flush=True)
-    return torch.clip(x_t, -1, 1)
+    return torch.clip(x_t, -1, 1), x_t  # (the reference's return value; and x_0 before its clip)
 
 
 def main():
@@ -111,9 +113,9 @@ def main():
             per, shape = 3 * 32 * 32, (3, 32, 32)
             x_T, _ = candidates("random", seed, rnd, cands, per, shape)
             print("full_C2", flush=True)
-            x0 = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
+            x0, raw = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
             G.save("full_C2", seed=seed, round=rnd, n=256, cands=np.array(cands), T=T, beta_T=0.02, x_T=x_T, x0=x0,
-                   scores=score(x0))
+                   x0_raw=raw, scores=score(x0))
         if "C3" in only:
             a, T, seed, rnd, cands, w, lab = ARCH_C, 1000, 41, 1, (0, 31), 1.8, 3
             per, shape = 3 * 32 * 32, (3, 32, 32)
@@ -121,25 +123,25 @@ def main():
             net = G.ref_cfg(MC, a, synthetic_state_dict(a, 0))
             smp = DC.GaussianDiffusionSampler(net, 1e-4, 0.028, T, w=w)
             print("full_C3", flush=True)
-            x0 = drive(smp, x_T, run_key(seed, rnd), cands, per, T, labels=torch.full((len(cands),), lab))
+            x0, raw = drive(smp, x_T, run_key(seed, rnd), cands, per, T, labels=torch.full((len(cands),), lab))
             G.save("full_C3", seed=seed, round=rnd, n=32, cands=np.array(cands), T=T, beta_T=0.028, w=w, label=lab,
-                   scale=np.float32(1 - 0.95), x_T=x_T, pivot=pivot, x0=x0, scores=score(x0))
+                   scale=np.float32(1 - 0.95), x_T=x_T, pivot=pivot, x0=x0, x0_raw=raw, scores=score(x0))
         if "C4" in only:
             a, T, seed, rnd, cands = dataclasses.replace(ARCH_A, img_size=64), 1000, 42, 0, (0, 15)
             per, shape = 3 * 64 * 64, (3, 64, 64)
             x_T, _ = candidates("random", seed, rnd, cands, per, shape)
             print("full_C4", flush=True)
-            x0 = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
+            x0, raw = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
             G.save("full_C4", seed=seed, round=rnd, n=16, cands=np.array(cands), T=T, beta_T=0.02, x_T=x_T, x0=x0,
-                   scores=score(x0))
+                   x0_raw=raw, scores=score(x0))
         if "C5" in only:
             a, T, seed, rnd, cands = dataclasses.replace(ARCH_A, T=3000), 3000, 33, 0, (0, 64, 127)
             per, shape = 3 * 32 * 32, (3, 32, 32)
             x_T, pivot = candidates("path", seed, rnd, cands, per, shape, scale=0.1)
             print("full_C5", flush=True)
-            x0 = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
+            x0, raw = drive(ddpm(a, T, 0.02), x_T, run_key(seed, rnd), cands, per, T)
             G.save("full_C5", seed=seed, round=rnd, n=128, cands=np.array(cands), T=T, beta_T=0.02,
-                   scale=np.float32(0.1), x_T=x_T, pivot=pivot, x0=x0, scores=score(x0))
+                   scale=np.float32(0.1), x_T=x_T, pivot=pivot, x0=x0, x0_raw=raw, scores=score(x0))
     print("torch", torch.__version__)
 
 
