@@ -1450,7 +1450,9 @@ template <> struct GnpCfg<8> { static constexpr int NSEG = 4, ITEMS = 13, RES = 
 #define ITSD_P4_ZR8 1  // COMPACT 16x16x32 forms: 8 zero rows (a padding lane keeps its bank slot; 0: one, A/B builds)
 #endif
 #ifndef ITSD_P5_SC_LAUNCH
-#define ITSD_P5_SC_LAUNCH 5.0  // the standalone 1x1 launch a folded shortcut saves, in p5 chunk-times (3: r05aq A/B)
+#define ITSD_P5_SC_LAUNCH 7.5  // the standalone 1x1 launch a folded shortcut saves, in p5 chunk-times: round 5's 5 (3:
+                               // r05aq A/B) + the 2.4 by which round 6 re-priced a 2-slice combine (0.6 -> 3.0), so
+                               // that the folds round 5 measured faster stay chosen
 #endif
 #ifndef ITSD_P5_SWZ
 #define ITSD_P5_SWZ 1  // conv3x3_gn_p5_kernel's per-level halo swizzle at W <= 16 (0: (h >> 1) & 7; A/B builds)
@@ -2634,11 +2636,15 @@ constexpr int P5_BD = ITSD_P5_BD;    // B fragment buffers (reads two k-steps = 
 // items waves w and w + 2 share a 32-cout block and each takes two of the four 32-pixel blocks: the same k order per
 // output and the same statistics tree, so the forward is bit-identical to 128-cout items; twice the items at the same
 // K slices -- the 4x4 level at N = 256 fills the 256 CUs without splitting K (128 tiles of 128 couts)
-template <int W, int CB = 128>
+// DIST (round 6): the split-K combine shared by every slice (ConvArgs::kdist; a separate instantiation, so the
+// last-arriver form's code is the round-5 kernel's: sharing one body cost its launches 5 % at N = 256,
+// profiles/r06/census_r05lib_vs_r06_r06k.txt)
+template <int W, int CB = 128, bool DIST = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   typedef bf16_t T;
   using Cf = Gp5Cfg<W>;
   static_assert(CB == 128 || (CB == 64 && W <= 8), "p5 cout tile");
+  static_assert(!DIST || CB == 128, "shared combine: 128-cout items");
   constexpr int CWB = CB / 32, NJW = CWB;  // 32-cout blocks a tile; 32-pixel blocks a wave (4 waves: CWB x 4 / CWB)
   constexpr int HW = Cf::HW, NSEG = Cf::NSEG, W2 = Cf::W2, HS = Cf::HS, TPS = Cf::TPS, RPP = Cf::RPP;
   constexpr int ITEMS = Cf::ITEMS, HALO = Cf::HALO, TH = Cf::TH, HY0 = Cf::HY0, NHY = Cf::NHY;
@@ -2701,7 +2707,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   if (wid < 4) {
     // ================================================================ MFMA waves
     const int rl = lane & 31, hh = lane >> 5;
-    const int cw = wid % CWB, jb0 = (wid / CWB) * NJW;  // this wave's 32-cout block and first 32-pixel block
+    const int cw = CB == 128 ? wid : wid % CWB, jb0 = CB == 128 ? 0 : (wid / CWB) * NJW;  // its 32-cout block, first px block
     int hb[NJW];  // halo row of this lane's pixel (tap 0, 0) in each of its 32-pixel blocks
     int hq[NJW];  // its swz coordinates SC1 y + SC2 x (W <= 16)
 #pragma unroll
@@ -2907,7 +2913,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
                       __float_as_uint(acc[j][4 * g + 3])},
                 slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (CB == 128 && a.kdist) {
+        if constexpr (DIST) {
           // ---- the combine shared by all ST slices (every block runs one item: the grid is co-resident). The wave's
           // 16 (pixel block j, cout group g) units of 32 px x 8 couts form NU statistics units of NJ pixel blocks (one
           // consumer GroupNorm slot each: W = 4 a half block, W = 8 a pair, W >= 16 the tile); slice z finishes units
@@ -3073,7 +3079,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         }
         }  // (last arriver)
       }
-      if (!a.kdist) TL(3);
+      if constexpr (!DIST) TL(3);
       // ---- epilogue: out = acc + addv + residual (lane: pixel 32j + rl, couts 32w + 8g + 4hh + e)
       const int tileP = tp * 128, tileC = tc * CB;
       const float* av = addv + (k & 1) * NSEG * CONV_BM + cw * 32 + 4 * hh;
@@ -3172,7 +3178,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
         }
       }
-      if (!a.kdist) TL(4);
+      if constexpr (!DIST) TL(4);
     }
     TL(5);
     return;
@@ -3738,13 +3744,15 @@ bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 |
 static bool p5_dist(int tiles, int st) {
   return g_p5_dist && st > 2 && st <= 16 && (long long)tiles * st <= g_num_cus && (long long)tiles * 4 * 32 <= kTicketCap;
 }
-// its cost in chunk-times (a 64-channel chunk ~4.1 us at N <= 64), fitted to the per-op sweep of forced slice counts
-// (tools/p5_split_sweep.py, profiles/r06/p5_split_n*_r06f.txt): every split pays the partial's write-through and
-// drain, the arrival and the slab reads before its epilogue -- shared, ~2.5 (one poll, two overlapped slab round
-// trips); the last arriver ~2 + 0.5 a slice (its serial slice reads). (Round 5's 0.3 a slice over-split: the 16x16
-// level at N = 32 ran 2 slices at 25 us a launch where 1 takes 18.)
+// its cost in chunk-times (a 64-channel chunk ~4.1 us at N <= 64), fitted to the per-op sweeps of forced slice counts
+// (tools/p5_split_sweep.py, profiles/r06/p5_split_n*_r06f.txt, sweep256_r06m.txt): the last item's combine is
+// exposed at the end of the launch -- the partial's write-through and drain, the arrival, the slab reads, then the
+// epilogue: shared ~2.5 (one poll, two overlapped slab round trips), the last arriver ~2 + 0.5 a slice (its serial
+// slice reads). (Round 5 priced 0.3 a slice: it ran the 16x16 level at N = 32 on 2 slices, 25 us a launch where 1
+// takes 18; amortising it over a block's items instead ran N = 256's 4x4 level on 4 slices, 50-55 us against 36.)
 static double p5_combine_cost(int tiles, int st, int cb) {
-  return st <= 1 ? 0.0 : cb == 128 && p5_dist(tiles, st) ? 2.5 : 2.0 + 0.5 * st;
+  if (st <= 1) return 0.0;
+  return cb == 128 && p5_dist(tiles, st) ? 2.5 : 2.0 + 0.5 * st;
 }
 // 64-cout items (CB = 64, W <= 8): a chunk's MFMA work halves, its staging does not -- ITSD_P5_C64_CHUNK chunk-times
 #ifndef ITSD_P5_C64_CHUNK
@@ -3897,6 +3905,14 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   const int items = tiles * (p.s + p.s2);
   a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2);
   const dim3 g(std::min(items, g_num_cus));
+  if (a.kdist) {  // (items <= CUs: 128-cout tiles at W <= 32)
+    if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p5_kernel<32, 128, true>), g, dim3(512), 0, s, a);
+    else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p5_kernel<16, 128, true>), g, dim3(512), 0, s, a);
+    else if (a.Wout == 8) ITSD_LAUNCH((conv3x3_gn_p5_kernel<8, 128, true>), g, dim3(512), 0, s, a);
+    else if (a.Wout == 4) ITSD_LAUNCH((conv3x3_gn_p5_kernel<4, 128, true>), g, dim3(512), 0, s, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (a.Wout == 64) ITSD_LAUNCH(conv3x3_gn_p5_kernel<64>, g, dim3(512), 0, s, a);
   else if (a.Wout == 32) ITSD_LAUNCH(conv3x3_gn_p5_kernel<32>, g, dim3(512), 0, s, a);
   else if (a.Wout == 16) ITSD_LAUNCH(conv3x3_gn_p5_kernel<16>, g, dim3(512), 0, s, a);

@@ -351,9 +351,12 @@ __device__ __forceinline__ void atl(int slot) {
 
 // (round 4's 4-images-a-block form for the 4x4 middle block, S = 16, measured slower than the unfused ops
 // at N = 32 and equal at N = 256, was removed in round 5)
+#ifndef ITSD_ATTN_PF
+#define ITSD_ATTN_PF 8
+#endif
 template <int C>
 __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
-  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = 8;
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBW = CB / 4, NCH = C / 128, PF = ITSD_ATTN_PF;
   static_assert(C % 128 == 0, "C");
   constexpr int R_VT = S * C * 2, R_QK = R_VT + C * 128, R_GS = R_QK + 2 * S * 256, R_ST = R_GS + 32 * 2 * 4;
   __shared__ __attribute__((aligned(16))) char sm[R_ST + 2 * C * 2 * 4];
@@ -738,9 +741,12 @@ __global__ __launch_bounds__(512, 1) void attn_block_kernel(AttnBlockArgs a) {
 // only grow, by 12 per launch (12 / G per block), so a block's target -- the next multiple of 12 above the
 // value its own add returned -- holds whatever G earlier launches used (launches on a stream never overlap). Waiting blocks need the whole grid resident: the host launches it only when
 // n * G <= CUs (one 512-thread block per CU).
+#ifndef ITSD_ATTN_SPLIT_PF
+#define ITSD_ATTN_SPLIT_PF 8
+#endif
 template <int C, int G>
 __global__ __launch_bounds__(512, 1) void attn_block_split_kernel(AttnBlockArgs a) {
-  constexpr int S = 64, KS = C / 16, CB = C / 32, CBg = CB / G, CW = CBg * 32, PF = 8;
+  constexpr int S = 64, KS = C / 16, CB = C / 32, CBg = CB / G, CW = CBg * 32, PF = ITSD_ATTN_SPLIT_PF;
   static_assert(CB % G == 0 && C % 128 == 0 && 12 % G == 0, "G divides the channel blocks and 12");
   constexpr int QROW = CW * 2 + 16;  // Q_g / K_g row (bytes): padded so 16-B reads of 16 rows are conflict-free
   constexpr int R_VT = S * C * 2, R_Q = R_VT + CW * 128, R_K = R_Q + S * QROW, R_SM = R_K + S * QROW;

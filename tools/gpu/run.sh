@@ -7,7 +7,8 @@
 # steps:
 #   smoke                     __graft_entry__.smoke()
 #   tests[=f1,f2,...]         pytest -m gpu over tests/ (or the listed test files / node ids)
-#   stepab=N:V1,V2[:arch]     tools/step_ab.py: graph-replayed step time of option variants ("base", "k=v+k=v")
+#   stepab=N:V1,V2[:arch[:lib]]  tools/step_ab.py: graph-replayed step time of option variants ("base", "k=v+k=v"),
+#                             optionally of another build (ab_libs/libitsd_hip_<lib>.so)
 #   census=N[:arch]           tools/census.py per-launch census of one forward (arch a / c; c: N is the guided batch)
 #   timeline=N:op,op,...      tools/timeline.py p5 launch timelines (stamps build ab_libs/libitsd_hip_stamps.so)
 #   pmc=N                     PMC passes over one census forward + per-dispatch table + traffic files
@@ -31,9 +32,11 @@ for step in "$@"; do
       timeout -k 10 1100 python -u -m pytest $sel -m gpu -x -v -s --timeout 500 --timeout-method thread > "$log" 2>&1 || fail tests $? "$log"
       tail -1 "$log" ;;
     stepab)
-      IFS=: read -r n variants arch <<< "$arg"
-      timeout -k 10 400 python tools/step_ab.py --n "$n" --variants "$variants" --arch "${arch:-a}" > "$out/stepab_${arch:-a}$n.txt" 2>&1 || fail stepab $? "$out/stepab_${arch:-a}$n.txt"
-      tail -4 "$out/stepab_${arch:-a}$n.txt" ;;
+      IFS=: read -r n variants arch lib <<< "$arg"
+      f="$out/stepab_${arch:-a}$n${lib:+_$lib}.txt"
+      timeout -k 10 400 python tools/step_ab.py --n "$n" --variants "$variants" --arch "${arch:-a}" \
+        ${lib:+--lib ab_libs/libitsd_hip_$lib.so} > "$f" 2>&1 || fail stepab $? "$f"
+      tail -4 "$f" ;;
     census)
       IFS=: read -r n arch <<< "$arg"
       timeout -k 10 200 python tools/census.py --n "$n" --arch "${arch:-a}" > "$out/census_${arch:-a}$n.txt" 2>&1 || fail census $? "$out/census_${arch:-a}$n.txt" ;;
