@@ -50,12 +50,14 @@ bool p5_eligible(int H, int W);
 bool conv_p5_selected(const ConvArgs& a);
 bool conv_p4_selected(const ConvArgs& a);
 bool conv_p5_sc_fold(const ConvArgs& a);
+int conv_small_split(const ConvArgs& a);
 int conv_gn_wide_segs(int H, int W, int M, int Cout, bool any_tiles = false);
 hipError_t launch_gn_coef(const GNArgs&, int, float*, hipStream_t);
 hipError_t launch_head_mfma(const HeadArgs&, hipStream_t);
 hipError_t launch_tail_mfma(const TailArgs&, hipStream_t);
 bool tail_mfma_ok(int H, int W, int C);
 int g_io_mfma = 1;  // bf16 head / tail on MFMA (itsd_set_option "io_mfma", read at create)
+int g_small_gn = 1;  // conv_small writes its consumer GroupNorm's output (itsd_set_option "small_gn"): 0 off, 1 on
 hipError_t launch_noise(float*, const float*, int, long long, float, unsigned long long, unsigned, long long,
                         hipStream_t);
 template <typename T> hipError_t launch_nhwc_to_nchw(const void*, float*, int, int, int, hipStream_t);
@@ -138,6 +140,9 @@ struct Op {
   // sc_*): on block2, the shortcut op, its weights in fragment order and the two biases summed; on the shortcut, block2
   int sc_op = -1, sc_into = -1;
   size_t sc_wfrag = SIZE_MAX, bias_sc = SIZE_MAX;
+  // a conv and the GroupNorm op right after it over its output alone (conv_small writes the GroupNorm's output in its
+  // epilogue, ConvArgs gn_out): on the conv, the GN op; on the GN op, the conv
+  int gn_next = -1, gn_from = -1;
 };
 
 // Host staging for the weight arena: fp32 params and packed conv weights.
@@ -829,6 +834,17 @@ int build(itsd_unet* u, const itsd_tensor_view* views, int nviews) {
     return fail(ITSD_ERR_WEIGHTS, "state_dict has " + std::to_string(nviews) + " entries, model uses " +
                                       std::to_string(b.used) + " (unexpected keys present)");
   }
+  // a GroupNorm op over the output of the conv right before it (and nothing else): a candidate for conv_small's fused
+  // GroupNorm output (conv_args decides per launch; every activation has its own buffer, so the GroupNorm's output
+  // never aliases the conv's operands)
+  for (size_t i = 1; i < u->ops.size(); ++i) {
+    Op& g = u->ops[i];
+    Op& p = u->ops[i - 1];
+    if (g.kind == OP_GN && g.src2 < 0 && p.kind == OP_CONV && p.dst == g.src1 && p.sc_into < 0 && p.vt < 0) {
+      p.gn_next = (int)i;
+      g.gn_from = (int)i - 1;
+    }
+  }
   // channel-statistics slabs for every tensor a GroupNorm reads (written by its producer)
   {
     std::vector<int> need;
@@ -958,6 +974,20 @@ int conv_args(itsd_unet* u, const Op& o, const RunCtx& c, ConvArgs& a) {
     a.gn_spi2 = o.src2 >= 0 ? u->acts[o.src2].spi : 0;
     a.gn_gamma = u->wp(o.gn_gamma);
     a.gn_beta = u->wp(o.gn_beta);
+  }
+  // (round 6) the consumer GroupNorm(+SiLU) in conv_small's epilogue (run_program then skips the GN op): whole-image
+  // tiles with one statistics slot an image (HWo <= 16: the CFG model's 2x2 / 1x1 levels), a group's gs = Cout / 32
+  // channels inside one 64-cout tile
+  if (o.gn_next >= 0 && itsd::g_small_gn && u->bf16 && a.stats && !a.gn_coef && !o.subpix && !a.vt_out &&
+      u->acts[o.dst].spi == 0) {
+    const int HWo = a.Hout * a.Wout, gs = a.Cout / 32;
+    if (HWo <= 16 && 64 % HWo == 0 && a.Cout % 64 == 0 && gs >= 2 && 64 % gs == 0 && conv_small_split(a)) {
+      const Op& g = u->ops[o.gn_next];
+      a.gn_out = u->ap(g.dst);
+      a.go_gamma = u->wp(g.gamma);
+      a.go_beta = u->wp(g.beta);
+      a.go_silu = g.silu;
+    }
   }
   if (o.sc_op >= 0 && itsd::g_p5_sc) {  // the shortcut folded in (run_program then skips the shortcut's launch)
     const Op& sc = u->ops[o.sc_op];
@@ -1109,6 +1139,10 @@ int run_program(itsd_unet* u, const RunCtx& c, hipStream_t s) {
     if (o.kind == OP_GNCOEF && oi + 1 < u->ops.size() && u->ops[oi + 1].kind == OP_CONV) {
       ConvArgs na{};  // gn_fold: the consumer conv finalizes this GroupNorm itself
       if (conv_args(u, u->ops[oi + 1], c, na) == ITSD_OK && na.gn_fold) continue;
+    }
+    if (o.kind == OP_GN && o.gn_from >= 0) {
+      ConvArgs na{};  // a GroupNorm its producer conv wrote in its epilogue
+      if (conv_args(u, u->ops[o.gn_from], c, na) == ITSD_OK && na.gn_out) continue;
     }
     if (o.kind == OP_CONV && o.sc_into >= 0) {
       ConvArgs na{};  // a shortcut its block2 conv runs as K slices
@@ -1385,6 +1419,11 @@ int itsd_set_option(const char* key, int value) {
   if (!std::strcmp(key, "p5_sc")) {  // ResBlock 1x1 shortcuts as K slices of their block2 p5 conv: 0 off, 1 auto, 2 always
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_sc in [0,2]");
     itsd::g_p5_sc = value;
+    return ITSD_OK;
+  }
+  if (!std::strcmp(key, "small_gn")) {  // conv_small writes its consumer GroupNorm's output (the GN launch skipped): 0 off, 1 on
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "small_gn in [0,1]");
+    itsd::g_small_gn = value;
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p5_dist")) {  // p5's split-K combine shared by every slice (co-resident grids): 0 off (last arriver),

@@ -176,6 +176,14 @@ struct ConvArgs {
   int kdist;
   int* err;
   int spin_bound;
+  // conv_small (whole-image tiles, HWo <= 16) with its consumer GroupNorm(+SiLU) fused into the epilogue: the next op
+  // (gn_apply_kernel over this output alone) is skipped and the epilogue writes silu(GN(out)) to gn_out as well, from
+  // the same per-channel slot sums and the same fp64 group finalize (bit-identical); a group's channels lie inside
+  // one 64-cout tile (host: 64 % (Cout / 32) == 0). Null: no fused GroupNorm
+  void* gn_out;
+  const float* go_gamma;
+  const float* go_beta;
+  int go_silu;
 };
 
 // Channel-statistics slab of an NHWC tensor (written by its producer): slots of

@@ -165,8 +165,9 @@ __device__ __forceinline__ long long temb_row_of(const ConvArgs& a) {
 // couts); a tile holding more images (the 2x2 / 1x1 levels: 32 / 128 images per 128-pixel tile)
 // reads its rows from global memory per output chunk instead.
 // PRE: the caller has already written the additive rows to LDS (E + BN * ER).
+// GNO: the kernel may carry a fused consumer GroupNorm (ConvArgs gn_out; conv_small only).
 template <typename T, int BM = 128, int BN = 128, int NTH = 256, int ADDV = (EPI_BYTES - 128 * EROW * 4) / 4,
-          bool PRE = false>
+          bool PRE = false, bool GNO = false>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
 
 // accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
@@ -184,6 +185,86 @@ __device__ __forceinline__ void acc_to_E(f32x16 (&acc)[2][2], float* E, int pbas
       }
 }
 
+// The consumer GroupNorm(+SiLU) of a whole-image tile (ConvArgs gn_out: HWo <= 16, one statistics slot an image, every
+// group's gs = Cout / 32 channels inside the tile), from E holding the rounded outputs (the statistics pass ran). The
+// (image, group) statistics are gn_apply_kernel's to the bit: the per-channel slot sums in the statistics pass's order
+// (float sum, fmaf square sum over the slot's pixels), eight fp64 partials -- partial l adds channels l, l + 8, .. in
+// order, as lane l8 = l of gn_apply's 8-lane group -- combined in its xor-butterfly's tree ((p0+p1)+(p2+p3)) +
+// ((p4+p5)+(p6+p7)), mean / rstd rounded to float; here one thread per (image, group), so the finalize is one short
+// pass instead of gn_apply's shuffle rounds. The outputs get gn_apply's coefficient expressions: silu(x (rstd gamma) +
+// (beta - mean rstd gamma)), one bf16 rounding. gst: 2 floats a pair of LDS (free: the additive rows are dead after
+// the output pass).
+template <typename T, int BM, int BN>
+__device__ __forceinline__ void gn_out_from_E(const ConvArgs& a, const float* E, float* gst, int tileP, int tileC) {
+  constexpr int ER = BM + 4, EPC = 16 / (int)sizeof(T), CPR = BM / EPC;
+  static_assert(EPC == 8, "bf16 chunks");
+  const int tid = threadIdx.x, NT = blockDim.x;
+  const int HWo = a.Hout * a.Wout, gs = a.Cout / 32;
+  const int nimg = BN / HWo, ngrp = BM / gs, npairs = nimg * ngrp;
+  const int img0 = tileP / HWo;
+  // this thread's output chunk columns (the same for every row it stores: NT % CPR == 0): gamma / beta issued first
+  const int cl = (tid % CPR) * EPC, co = tileC + cl;
+  f32x4 gam[2], bet[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    gam[q] = co < a.Cout ? *(const f32x4*)(a.go_gamma + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bet[q] = co < a.Cout ? *(const f32x4*)(a.go_beta + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // (no barrier here: the statistics pass's own barrier -- host: a.stats -- already follows the output pass's last
+  // reads of the additive rows)
+  for (int pr = tid; pr < npairs; pr += NT) {
+    const int il = pr / ngrp, gl = pr - il * ngrp;
+    if ((img0 + il) * HWo >= a.M) continue;
+    double ps[8], pq[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      ps[l] = 0.0;
+      pq[l] = 0.0;
+      for (int k = l; k < gs; k += 8) {
+        const int c = gl * gs + k;
+        float sum = 0.f, sq = 0.f;
+        for (int j = 0; j < HWo; ++j) {
+          const float v = E[(il * HWo + j) * ER + c];
+          sum += v;
+          sq = fmaf(v, v, sq);
+        }
+        ps[l] += (double)sum;
+        pq[l] += (double)sq;
+      }
+    }
+    const double sd = ((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7]));
+    const double qd = ((pq[0] + pq[1]) + (pq[2] + pq[3])) + ((pq[4] + pq[5]) + (pq[6] + pq[7]));
+    const double En = (double)gs * HWo;
+    const double mean = sd / En;
+    double var = qd / En - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    gst[2 * pr] = (float)mean;
+    gst[2 * pr + 1] = (float)(1.0 / sqrt(var + (double)1e-5f));
+  }
+  // LDS writes drained, then the block barrier alone (a __syncthreads would also wait for the gamma / beta loads)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // (keeps the gst reads below the barrier)
+  if (co >= a.Cout) return;
+  for (int pl = tid / CPR; pl < BN; pl += NT / CPR) {
+    const int p = tileP + pl;
+    if (p >= a.M) break;
+    const int il = pl / HWo;
+    u32x4 y;
+    T* ye = (T*)&y;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const int pr = il * ngrp + (cl + e) / gs;
+      const float sc = gst[2 * pr + 1] * gam[e >> 2][e & 3];
+      const float c0 = sc, c1 = bet[e >> 2][e & 3] - gst[2 * pr] * sc;
+      float v = E[pl * ER + cl + e] * c0 + c1;  // (E: the rounded outputs, host: a.stats)
+      if (a.go_silu) v = silu(v);
+      ye[e] = Elem<T>::to(v);
+    }
+    *(u32x4*)((T*)a.gn_out + (size_t)p * a.Cout + co) = y;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2][2], char* smem, int tileP,
                                               int tileC, int phase = -1) {
@@ -194,7 +275,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
 
 // E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
 // and the consumer GroupNorm's statistics slab.
-template <typename T, int BM, int BN, int NTH, int ADDV, bool PRE>
+template <typename T, int BM, int BN, int NTH, int ADDV, bool PRE, bool GNO>
 __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int ER = BM + 4;  // E row (floats): 128x128 tile -> EROW
@@ -378,6 +459,9 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
         *(f32x4*)(a.stats + (slot * 2 + 1) * a.Cout + co) = sq;
       }
     }
+  }
+  if constexpr (GNO) {
+    if (a.gn_out) gn_out_from_E<T, BM, BN>(a, E, E + BN * ER, tileP, tileC);
   }
 }
 
@@ -827,7 +911,7 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       if (tid + 256 * u < nent) addv[tid + 256 * u] = pre[u];
   }
   __syncthreads();
-  epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true>(a, smem, tileP, tileC, -1);
+  epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true, true>(a, smem, tileP, tileC, -1);
 }
 
 // ---------------------------------------------------------------------------- streaming 1x1
@@ -3945,8 +4029,53 @@ static hipError_t launch_p4_ablation(const ConvArgs& a, dim3 gp, hipStream_t s) 
 
 #endif
 
+// conv_small's K slices when launch_conv runs this (bf16, statistics-free or whole-image) conv on it, else 0 (shared
+// by launch_conv and the host's GroupNorm-output fusion, api.hip conv_args, so that both see one decision).
+int conv_small_split(const ConvArgs& a) {
+  if (a.gn_coef || conv_p4_plain_selected(a)) return 0;
+  if (g_conv1x1 && conv1x1_stream_ok(a)) {
+    const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
+    const int G = (g_num_cus / (8 * nTC)) * 8 * nTC;
+    if (G > 0 && (long long)nTP * nTC >= 4LL * G) return 0;
+  }
+  const dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
+  // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
+  // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
+  // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured
+  // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt)
+  // Under ~one block per CU (the 2x2 / 1x1 levels, small batches) conv_small splits K itself
+  // (in-launch combine), up to ~2 blocks per CU with >= 2 K-chunks a slice.
+  const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
+  int S = 1;
+  // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
+  // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip; not
+  // for K >= 7168: the CFG's merged 5x5 DownSample into 8x8, K = 12800 at 2N = 64, measured 156 us on
+  // conv_small's 64x64 tiles vs 97 us on the 128-tile pipe, profiles/r04/census_archC_2N64_small8_k.txt)
+  const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
+  // (round 5: also where the 128-tile grid's last round is part-empty -- N = 256's 8x8 shortcuts, 384 tiles --
+  // measured 31 -> 48 us a launch, N = 256 step +0.8 %, profiles/r05/small8_part_round_r05t.txt: not taken)
+  const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256 &&
+                      a.K < 7168;
+  if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
+      (a.Hout * a.Wout <= 16 || wide || small8) &&
+      gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
+    const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
+    S = std::min(std::min((512 + blocks - 1) / blocks, nK / g_small_minks), 16);  // <= 2 combine batches
+    while (S > 1 && (long long)blocks * S * 4096 > a.splitk_cap) --S;
+    if (S < 1) S = 1;
+  }
+  if (g_small_conv && conv_small_ok(a) &&
+      (g_small_conv == 2 || S > 1 || wide || small8 ||
+       (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
+    return S;
+  }
+  return 0;
+}
+
 template <typename T>
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
+  // (the consumer GroupNorm's output is written by conv_small's epilogue only: host sets gn_out where it runs)
+  if (a.gn_out && (sizeof(T) != 2 || !conv_small_split(a))) return hipErrorInvalidValue;
   if constexpr (sizeof(T) == 2) {
     if (a.gn_coef) {
       // the 4x4 level always (no other fused kernel holds it); the others where p4 under-fills the chip
@@ -4006,35 +4135,8 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
         return hipGetLastError();
       }
     }
-    // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
-    // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
-    // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured
-    // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt)
-    // Under ~one block per CU (the 2x2 / 1x1 levels, small batches) conv_small splits K itself
-    // (in-launch combine), up to ~2 blocks per CU with >= 2 K-chunks a slice.
-    dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
-    int S = 1;
-    // (wide: a statistics-free conv of larger images whose 128x128 grid under-fills the chip)
-    // (small8: the 8x8 level's convs -- down, shortcuts -- when the 128x128 grid under-fills the chip; not
-    // for K >= 7168: the CFG's merged 5x5 DownSample into 8x8, K = 12800 at 2N = 64, measured 156 us on
-    // conv_small's 64x64 tiles vs 97 us on the 128-tile pipe, profiles/r04/census_archC_2N64_small8_k.txt)
-    const bool wide = g_small_wide && a.Hout * a.Wout > SM_B && grid.x * grid.y < (g_small_wide == 2 ? 512u : 256u);
-    // (round 5: also where the 128-tile grid's last round is part-empty -- N = 256's 8x8 shortcuts, 384 tiles --
-    // measured 31 -> 48 us a launch, N = 256 step +0.8 %, profiles/r05/small8_part_round_r05t.txt: not taken)
-    const bool small8 = g_small_8x8 && a.Hout * a.Wout > 16 && a.Hout * a.Wout <= SM_B && grid.x * grid.y < 256 &&
-                        a.K < 7168;
-    if (g_small_conv && conv_small_ok(a) && a.splitk_ws && a.tickets && g_splitk &&
-        (a.Hout * a.Wout <= 16 || wide || small8) &&
-        gs.x * gs.y < 256 && gs.x * gs.y <= kTicketCap) {
-      const int blocks = (int)(gs.x * gs.y), nK = a.ksize * a.ksize * ((a.C1 + a.C2) / 64);
-      S = std::min(std::min((512 + blocks - 1) / blocks, nK / g_small_minks), 16);  // <= 2 combine batches
-      while (S > 1 && (long long)blocks * S * 4096 > a.splitk_cap) --S;
-      if (S < 1) S = 1;
-    }
-    if (g_small_conv && conv_small_ok(a) &&
-        (g_small_conv == 2 || S > 1 || wide || small8 ||
-         (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
-      gs.z = S;
+    if (const int S = conv_small_split(a)) {
+      const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B, S);
       ITSD_LAUNCH(conv_small<false>, gs, dim3(256), 0, s, a);
       return hipGetLastError();
     }
