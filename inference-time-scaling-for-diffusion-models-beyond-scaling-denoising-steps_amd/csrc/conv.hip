@@ -168,7 +168,8 @@ __device__ __forceinline__ long long temb_row_of(const ConvArgs& a) {
 // GNO: the kernel may carry a fused consumer GroupNorm (ConvArgs gn_out; conv_small only).
 template <typename T, int BM = 128, int BN = 128, int NTH = 256, int ADDV = (EPI_BYTES - 128 * EROW * 4) / 4,
           bool PRE = false, bool GNO = false>
-__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase);
+__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase,
+                                                const f32x4* gn_affine = nullptr);
 
 // accumulators (waves 0..3, 2x2 of 64x64) -> fp32 tile E[pixel][cout] in LDS
 __device__ __forceinline__ void acc_to_E(f32x16 (&acc)[2][2], float* E, int pbase) {
@@ -185,6 +186,18 @@ __device__ __forceinline__ void acc_to_E(f32x16 (&acc)[2][2], float* E, int pbas
       }
 }
 
+// gamma / beta of the 8 output channels thread tid stores in gn_out_from_E (BM / 8 chunks a row)
+template <int BM>
+__device__ __forceinline__ void gn_affine_of(const ConvArgs& a, int tileC, f32x4 (&gam)[2], f32x4 (&bet)[2]) {
+  const int co = tileC + (threadIdx.x % (BM / 8)) * 8;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const bool ok = a.gn_out && co < a.Cout;
+    gam[q] = ok ? *(const f32x4*)(a.go_gamma + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bet[q] = ok ? *(const f32x4*)(a.go_beta + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 // The consumer GroupNorm(+SiLU) of a whole-image tile (ConvArgs gn_out: HWo <= 16, one statistics slot an image, every
 // group's gs = Cout / 32 channels inside the tile), from E holding the rounded outputs (the statistics pass ran). The
 // (image, group) statistics are gn_apply_kernel's to the bit: the per-channel slot sums in the statistics pass's order
@@ -195,21 +208,17 @@ __device__ __forceinline__ void acc_to_E(f32x16 (&acc)[2][2], float* E, int pbas
 // (beta - mean rstd gamma)), one bf16 rounding. gst: 2 floats a pair of LDS (free: the additive rows are dead after
 // the output pass).
 template <typename T, int BM, int BN>
-__device__ __forceinline__ void gn_out_from_E(const ConvArgs& a, const float* E, float* gst, int tileP, int tileC) {
+__device__ __forceinline__ void gn_out_from_E(const ConvArgs& a, const float* E, float* gst, int tileP, int tileC,
+                                              const f32x4 (&gam)[2], const f32x4 (&bet)[2]) {
   constexpr int ER = BM + 4, EPC = 16 / (int)sizeof(T), CPR = BM / EPC;
   static_assert(EPC == 8, "bf16 chunks");
   const int tid = threadIdx.x, NT = blockDim.x;
   const int HWo = a.Hout * a.Wout, gs = a.Cout / 32;
   const int nimg = BN / HWo, ngrp = BM / gs, npairs = nimg * ngrp;
   const int img0 = tileP / HWo;
-  // this thread's output chunk columns (the same for every row it stores: NT % CPR == 0): gamma / beta issued first
+  // this thread's output chunk columns (the same for every row it stores: NT % CPR == 0), whose gamma / beta the
+  // kernel loaded before its K loop (gn_affine_of)
   const int cl = (tid % CPR) * EPC, co = tileC + cl;
-  f32x4 gam[2], bet[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    gam[q] = co < a.Cout ? *(const f32x4*)(a.go_gamma + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-    bet[q] = co < a.Cout ? *(const f32x4*)(a.go_beta + co + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   // (no barrier here: the statistics pass's own barrier -- host: a.stats -- already follows the output pass's last
   // reads of the additive rows)
   for (int pr = tid; pr < npairs; pr += NT) {
@@ -276,7 +285,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
 // E (128 pixels x 128 couts, fp32, barrier passed) -> outputs (+ bias/temb/cemb/resid),
 // and the consumer GroupNorm's statistics slab.
 template <typename T, int BM, int BN, int NTH, int ADDV, bool PRE, bool GNO>
-__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase) {
+__device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, int tileP, int tileC, int phase,
+                                                const f32x4* gn_affine) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int ER = BM + 4;  // E row (floats): 128x128 tile -> EROW
   const int NT = blockDim.x;
@@ -460,8 +470,10 @@ __device__ __forceinline__ void epilogue_from_E(const ConvArgs& a, char* smem, i
       }
     }
   }
-  if constexpr (GNO) {
-    if (a.gn_out) gn_out_from_E<T, BM, BN>(a, E, E + BN * ER, tileP, tileC);
+  if constexpr (GNO) {  // (gn_affine: gamma[0..1], beta[2..3] of the thread's 8 channels, gn_affine_of)
+    if (a.gn_out)
+      gn_out_from_E<T, BM, BN>(a, E, E + BN * ER, tileP, tileC, *(const f32x4(*)[2])gn_affine,
+                               *(const f32x4(*)[2])(gn_affine + 2));
   }
 }
 
@@ -800,6 +812,9 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       pre[8 + u] = v1[u];
     }
   }
+  // the fused consumer GroupNorm's affine (gn_out), loaded with the additive rows
+  f32x4 gnab[4];
+  gn_affine_of<SM_B>(a, tileC, *(f32x4(*)[2])gnab, *(f32x4(*)[2])(gnab + 2));
   const int ntap = a.ksize * a.ksize;
   const int S = gridDim.z, kc0 = bt.z * nK / S, nKs = (bt.z + 1) * nK / S - kc0;
   auto issue = [&](int kc, int slot) {
@@ -911,7 +926,8 @@ __global__ __launch_bounds__(256, 2) void conv_small(ConvArgs a) {
       if (tid + 256 * u < nent) addv[tid + 256 * u] = pre[u];
   }
   __syncthreads();
-  epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true, true>(a, smem, tileP, tileC, -1);
+  epilogue_from_E<T, SM_B, SM_B, 256, (SM_SMEM - SM_B * (SM_B + 4) * 4) / 4, true, true>(a, smem, tileP, tileC, -1,
+                                                                                          gnab);
 }
 
 // ---------------------------------------------------------------------------- streaming 1x1
@@ -3825,8 +3841,9 @@ bool p5_eligible(int H, int W) { return H == W && (W == 4 || W == 8 || W == 16 |
 // +1 % at N = 256, whose 4x4 launches move 2 x 8 MB of partials: the last arriver's two serial reads cost no more than
 // the shared form's poll and staging, profiles/r06/stepab_a256_r06b.txt). g_p5_dist 2: planned
 // as shared, combined by the last arriver (the parity tests' bit-identity reference for the same plan)
-static bool p5_dist(int tiles, int st) {
-  return g_p5_dist && st > 2 && st <= 16 && (long long)tiles * st <= g_num_cus && (long long)tiles * 4 * 32 <= kTicketCap;
+// (not at the 64x64 level: its instantiation stays the last-arriver form, and the C4 shard's 512+ tiles are not co-resident)
+static bool p5_dist(int tiles, int st, int W) {
+  return g_p5_dist && W <= 32 && st > 2 && st <= 16 && (long long)tiles * st <= g_num_cus && (long long)tiles * 4 * 32 <= kTicketCap;
 }
 // its cost in chunk-times (a 64-channel chunk ~4.1 us at N <= 64), fitted to the per-op sweeps of forced slice counts
 // (tools/p5_split_sweep.py, profiles/r06/p5_split_n*_r06f.txt, sweep256_r06m.txt): the last item's combine is
@@ -3834,9 +3851,9 @@ static bool p5_dist(int tiles, int st) {
 // epilogue: shared ~2.5 (one poll, two overlapped slab round trips), the last arriver ~2 + 0.5 a slice (its serial
 // slice reads). (Round 5 priced 0.3 a slice: it ran the 16x16 level at N = 32 on 2 slices, 25 us a launch where 1
 // takes 18; amortising it over a block's items instead ran N = 256's 4x4 level on 4 slices, 50-55 us against 36.)
-static double p5_combine_cost(int tiles, int st, int cb) {
+static double p5_combine_cost(int tiles, int st, int cb, int W) {
   if (st <= 1) return 0.0;
-  return cb == 128 && p5_dist(tiles, st) ? 2.5 : 2.0 + 0.5 * st;
+  return cb == 128 && p5_dist(tiles, st, W) ? 2.5 : 2.0 + 0.5 * st;
 }
 // 64-cout items (CB = 64, W <= 8): a chunk's MFMA work halves, its staging does not -- ITSD_P5_C64_CHUNK chunk-times
 #ifndef ITSD_P5_C64_CHUNK
@@ -3853,7 +3870,7 @@ static int p5_split(const ConvArgs& a, int tiles, int nch, int cb, double fc) {
     double best = 1e30;
     for (int s = 1; s <= std::min(nch, 16); ++s) {
       const double waves = std::ceil((double)tiles * s / g_num_cus);
-      const double cost = waves * (std::ceil((double)nch / s) * fc + 1.5) + p5_combine_cost(tiles, s, cb);
+      const double cost = waves * (std::ceil((double)nch / s) * fc + 1.5) + p5_combine_cost(tiles, s, cb, a.Wout);
       if (cost < best - 1e-9) { best = cost; S = s; }
     }
   }
@@ -3947,7 +3964,7 @@ static P5Plan p5_plan(const ConvArgs& a) {
     auto cost = [&](int s, int s2) {
       const double waves = std::ceil((double)tiles * (s + s2) / g_num_cus);
       const double c3 = std::ceil((double)nch / s) * fc + 1.5, c1 = s2 ? 0.4 * std::ceil((double)nchx / s2) + 1.5 : 0.0;
-      return waves * std::max(c3, c1) + p5_combine_cost(tiles, s + s2, cb);
+      return waves * std::max(c3, c1) + p5_combine_cost(tiles, s + s2, cb, a.Wout);
     };
     P5Plan p;
     p.cb = cb;
@@ -3987,7 +4004,7 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   a.ksplit = p.s;
   a.sc_split = p.s2;
   const int items = tiles * (p.s + p.s2);
-  a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2);
+  a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2, a.Wout);
   const dim3 g(std::min(items, g_num_cus));
   if (a.kdist) {  // (items <= CUs: 128-cout tiles at W <= 32)
     if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p5_kernel<32, 128, true>), g, dim3(512), 0, s, a);

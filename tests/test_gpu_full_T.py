@@ -139,11 +139,14 @@ def _round(fx, net, smp, shape, kind, labels=None):
     pivot, scale = None, 1.0
     if kind != "random":
         pivot, scale = eng.initial_noise(shape), float(fx["scale"])
-        assert torch.equal(pivot.cpu(), torch.from_numpy(fx["pivot"]).reshape(shape))
+        # the device Philox normals against the host restatement the fixture was drawn with: within 2e-6
+        # (test_gpu_search.py::test_philox_noise_kernel_matches_oracle; log / cos differ by an ulp on a few elements)
+        dp = (pivot.cpu() - torch.from_numpy(fx["pivot"]).reshape(shape)).abs().max().item()
+        assert dp <= 2e-6, dp
     cands = [int(c) for c in fx["cands"]]
     xT = torch.cat([eng.candidate_noise(rnd, i, 1, shape, pivot=pivot, scale=scale) for i in cands]).cpu()
     dx = (xT - torch.from_numpy(fx["x_T"])).abs().max().item()
-    assert dx <= 1e-6, dx  # (the fused multiply-add's one rounding, emulated in fp64 on the host)
+    assert dx <= 4e-6, dx  # (the Philox bound above through pivot + scale z, one fp32 rounding emulated in fp64)
     r = eng.run_round(rnd, n, shape, pivot=pivot, scale=scale, labels=labels, kind=kind)
     # the same shard once more without the final clip (the synthetic model's images saturate to +-1: the pre-clip x0
     # is the continuous comparison): every candidate's trajectory is a function of (seed, global index) alone
