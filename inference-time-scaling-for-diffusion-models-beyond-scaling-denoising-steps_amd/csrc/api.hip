@@ -1426,6 +1426,12 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_small_gn = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "p5_pub")) {  // p5's two-slice last-arriver combine: 1 only the first arriver stores its partial,
+                                      // 0 both slices store theirs (round 5; bit-identity checks)
+    if (value < 0 || value > 1) return fail(ITSD_ERR_INVALID, "p5_pub in [0,1]");
+    itsd::g_p5_pub = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p5_dist")) {  // p5's split-K combine shared by every slice (co-resident grids): 0 off (last arriver),
                                        // 1 on, 2 the same plans as 1 combined by the last arriver (bit-identity checks)
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_dist in [0,2]");

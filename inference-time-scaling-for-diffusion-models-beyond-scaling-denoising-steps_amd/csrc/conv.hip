@@ -66,6 +66,7 @@ int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's 
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_p5_sc = 1;         // the ResBlock's 1x1 shortcut folded into its block2 p5 conv: 0 off, 1 auto (cost model), 2 always
+int g_p5_pub = 1;   // p5's two-slice last-arriver combine: only the first arriver stores its partial (0: both, round 5)
 int g_p5_dist = 1;       // p5's split-K combine shared by every slice of a tile where all items are co-resident (2: the
                          // same plans, combined by the last arriver)
 int g_gn_fold = 1;       // p5 finalizes its input GroupNorm itself (no gn_coef launch): 0 off, 1 on
@@ -3004,15 +3005,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         // slab [tile][slice][wave][NJW x 4 KB] (a wave's NJW pixel blocks x 4 cout groups of 1 KB)
         const uint32_t wbase = (uint32_t)(((size_t)tile * ST * 4 + wid) * NJW * 4096) + lane * 16;
         const uint32_t zstride = 4 * NJW * 4096;  // bytes between the slices of one (tile, wave)
+        auto store_partial = [&]() __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < NJW; ++j)
+          for (int j = 0; j < NJW; ++j)
 #pragma unroll
-          for (int g = 0; g < 4; ++g)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]), __float_as_uint(acc[j][4 * g + 2]),
-                      __float_as_uint(acc[j][4 * g + 3])},
-                slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int g = 0; g < 4; ++g)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]),
+                        __float_as_uint(acc[j][4 * g + 2]), __float_as_uint(acc[j][4 * g + 3])},
+                  slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
+        // (round 6) two slices, last-arriver form: arrival first; only the FIRST arriver stores its partial, the
+        // last one adds it to its own from registers (p0 + p1 == p1 + p0 in IEEE arithmetic: bit-identical to the
+        // slice-order sum). At N = 256's 4x4 level (256 items, S = 2) every block's combine runs at once and is
+        // bound by the slab bytes (16.8 MB written + 16.8 MB read a launch, ~7.5 us of the 45 us launch,
+        // profiles/r05/p5_timeline_n256_r05am.txt op 36): half of each
+        const bool pub2 = !DIST && a.kpub && ST == 2;  // (option p5_pub; 0: both slices publish, round 5)
+        if (!pub2) store_partial();
         if constexpr (DIST) {
           // ---- the combine shared by all ST slices (every block runs one item: the grid is co-resident). The wave's
           // 16 (pixel block j, cout group g) units of 32 px x 8 couts form NU statistics units of NJ pixel blocks (one
@@ -3158,6 +3168,57 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           }
           TL(5);
           return;
+        } else if (pub2) {
+          // counter per (tile, wave): arrivals in bits 0-7, the last arriver's give-up in bit 8, the first arriver's
+          // publication in bits 16+; whoever sees the other's final event resets it to 0 (the last arriver after the
+          // publication, or the publisher after a give-up), so the counter is 0 between launches on every path
+          int* const tk = a.tickets + tile * 4 + wid;
+          int old = 0;
+          if (lane == 0) old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          old = __builtin_amdgcn_readfirstlane(old);
+          if ((old & 0xff) == 0) {  // first: publish (R1: sc1 stores, drained, then the add) and go on
+            store_partial();
+            if (lane == 0) {
+              const int o2 = __hip_atomic_fetch_add(tk, 0x10000, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (o2 & 0x100) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            continue;
+          }
+          // last: wait for the publication (the first arriver is resident -- it took its ticket -- and waits on
+          // nothing, so this cannot hang on a grid larger than the chip; bounded anyway: a wait that runs out sets
+          // status bit 1 and poisons the tile with NaN, ITSD_ERR_HANDOFF)
+          int bad = 0;
+          if (lane == 0) {
+            int v = old + 1;
+            for (int it = 0; (v >> 16) == 0 && it < a.spin_bound; ++it) {
+              __builtin_amdgcn_s_sleep(1);
+              v = __hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if ((v >> 16) == 0) v = __hip_atomic_fetch_add(tk, 0x100, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bad = (v >> 16) == 0;  // (published meanwhile: the give-up's own return says so)
+            if (bad) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          bad = __builtin_amdgcn_readfirstlane(bad);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+#pragma unroll
+          for (int j = 0; j < NJW; ++j) {
+            u32x4 v[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              v[g] = __builtin_amdgcn_raw_buffer_load_b128(slab, wbase + (1 - z) * zstride + (j * 4 + g) * 1024, 0, 16);
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[j][4 * g + e] += __uint_as_float(v[g][e]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (bad) {
+#pragma unroll
+            for (int j = 0; j < NJW; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) acc[j][r] = __builtin_nanf("");
+          }
         } else {
         int old = 0;
         if (lane == 0) old = __hip_atomic_fetch_add(a.tickets + tile * 4 + wid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3188,9 +3249,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) s16[e] = q16[e] = 0.f;
       const char* rk = rres + (k & 1) * RTILE;  // this item's residual tile (halo waves, before the last barrier)
+      int rlo = rl;
+      asm volatile("" : "+v"(rlo));  // (the per-lane epilogue offsets rebuilt per item, not hoisted and spilled)
 #pragma unroll
       for (int j = 0; j < NJW; ++j) {
-        const int pl = (jb0 + j) * 32 + rl, seg = pl / SPX;
+        const int pl = (jb0 + j) * 32 + rlo, seg = pl / SPX;
         const bool live = Cf::ROWS ? tp * 128 < a.M : tp * NSEG + seg < nimg;
         const float* avj = av + seg * CB;
         uint32_t wv[4][2];
@@ -4005,6 +4068,7 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   a.sc_split = p.s2;
   const int items = tiles * (p.s + p.s2);
   a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2, a.Wout);
+  a.kpub = g_p5_pub;
   const dim3 g(std::min(items, g_num_cus));
   if (a.kdist) {  // (items <= CUs: 128-cout tiles at W <= 32)
     if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p5_kernel<32, 128, true>), g, dim3(512), 0, s, a);

@@ -77,6 +77,8 @@ int main() {
   expect("set_option p5_c64=2 (diagnostic)", itsd_set_option("p5_c64", 2), ITSD_ERR_INVALID);
   expect("set_option p5_dist=3", itsd_set_option("p5_dist", 3), ITSD_ERR_INVALID);
   expect("set_option p5_dist=1", itsd_set_option("p5_dist", 1), ITSD_OK);
+  expect("set_option p5_pub=2", itsd_set_option("p5_pub", 2), ITSD_ERR_INVALID);
+  expect("set_option p5_pub=1", itsd_set_option("p5_pub", 1), ITSD_OK);
   expect("set_option conv_variant=3 (removed)", itsd_set_option("conv_variant", 3), ITSD_ERR_INVALID);
   expect("set_option conv_variant=2 (default)", itsd_set_option("conv_variant", 2), ITSD_OK);
   expect("set_option spin_bound=-1", itsd_set_option("spin_bound", -1), ITSD_ERR_INVALID);

@@ -21,7 +21,7 @@ from itsd.weights import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 REL_L2_BF16 = 2e-2
-_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1, "p5_sc": 1}
+_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1, "p5_sc": 1, "p5_pub": 1}
 
 
 def _rel_l2(a, b):
@@ -114,3 +114,25 @@ def test_shared_combine_handoff_failure_is_loud():
     eps = net(xd, td).float().cpu()
     assert net.native(n).query("status") == 0 and torch.isfinite(eps).all()
     assert torch.equal(eps, _eps(net, xd, td, p5_dist=2))
+
+
+@pytest.mark.parametrize("n", [8, 16, 32, 64, 256, 5])
+def test_two_slice_publish_once_bit_identical(n):
+    """(round 6, option p5_pub) The two-slice last-arriver combine with only the FIRST arriver storing its partial
+    (arrival first; the last arriver adds the published partial to its own in registers: p0 + p1 == p1 + p0) against
+    both slices storing theirs (round 5): bit for bit, auto plans and every p5 level forced onto two slices
+    (p5 = 2, p5_split = 2, no shortcut fold, so every p5 launch takes the two-slice path); the counters stay
+    consistent run to run."""
+    net = _net()
+    x, t = _inputs(n, 6400 + n)
+    xd, td = x.cuda(), t.cuda()
+    for opts in ({}, {"p5": 2, "p5_split": 2, "p5_sc": 0}):
+        once = _eps(net, xd, td, **opts)
+        again = _eps(net, xd, td, **opts)
+        both = _eps(net, xd, td, p5_pub=0, **opts)
+        assert torch.isfinite(once).all()
+        assert torch.equal(once, again), opts
+        assert torch.equal(once, both), (opts, _rel_l2(once, both))
+        print(f"n={n} {opts}: publish-once == both-publish bit for bit")
+    rt.set_option("p5_pub", 1)
+    assert net.native(n).query("status") == 0

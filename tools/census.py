@@ -56,7 +56,7 @@ def main():
         defaults = {"conv_variant": 2, "splitk": 1, "small_conv": 1, "gn_wide": 1,
                     "p4_w": 7, "p5": 1, "p5_split": 0, "gn_fold": 1,
                     "small_wide": 1, "small_8x8": 1, "subpix_split": 1, "conv1x1": 1, "attn_wide": 1,
-                    "attn_wide_nq": 1, "attn_split": 1, "p4_sub": 1, "p4_plain": 1, "splitk_inl": 1, "convt_prune": 1, "p5_dist": 1, "small_gn": 1}
+                    "attn_wide_nq": 1, "attn_split": 1, "p4_sub": 1, "p4_plain": 1, "splitk_inl": 1, "convt_prune": 1, "p5_dist": 1, "p5_pub": 1, "small_gn": 1}
         # (diagnostic keys -- conv_dbg, small_minks, ... -- only where a variant names them: the shipped build refuses them)
         for rnd in range(3):
             for v in args.variants.split(","):
