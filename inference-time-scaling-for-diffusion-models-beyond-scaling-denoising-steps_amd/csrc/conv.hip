@@ -1049,11 +1049,23 @@ __global__ __launch_bounds__(256, 1) void conv1x1_stream_kernel(ConvArgs a) {
     // (the next tile's epilogue writes the out tile only after >= 1 more ring barrier)
   }
 }
+bool conv1x1_stream_ok(const ConvArgs& a);
+// conv1x1_stream_kernel's grid for this conv (whole XCD rounds of every cout tile), 0 where it does not run it: >= 4
+// pixel tiles a block, or (round 6) >= 1 where the 128-tile grid fills the chip by itself (N = 256's 8x8 shortcuts,
+// 384 tiles on 240 blocks: 19.7 -> 15.2 us a launch, step -0.5 %, profiles/r06/stepab_s1_mint_r06aa.txt); smaller
+// grids stay on conv_small's split-K path (small_wide)
+static int conv1x1_stream_grid(const ConvArgs& a) {
+  if (!g_conv1x1 || !conv1x1_stream_ok(a)) return 0;
+  const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
+  const int G = (g_num_cus / (8 * nTC)) * 8 * nTC;
+  const long long tiles = (long long)nTP * nTC;
+  return G > 0 && (tiles >= 4LL * G || (tiles >= G && tiles >= 256)) ? G : 0;
+}
 bool conv1x1_stream_ok(const ConvArgs& a) {
   const int Cin = a.C1 + a.C2;
   return a.zero && a.ksize == 1 && a.stride == 1 && a.pad == 0 && !a.subpix && !a.upsample && !a.zins && !a.gn_coef &&
          !a.stats && !a.temb && !a.cemb && !a.resid && !a.vt_out && a.C1 % 64 == 0 && a.C2 % 64 == 0 &&
-         (Cin == 256 || Cin == 384 || Cin == 512 || Cin == 640) && a.K == Cin && a.Cout % CONV_BM == 0 &&
+         (Cin == 128 || Cin == 256 || Cin == 384 || Cin == 512 || Cin == 640) && a.K == Cin && a.Cout % CONV_BM == 0 &&
          a.M % CONV_BN == 0;
 }
 
@@ -4114,11 +4126,7 @@ static hipError_t launch_p4_ablation(const ConvArgs& a, dim3 gp, hipStream_t s) 
 // by launch_conv and the host's GroupNorm-output fusion, api.hip conv_args, so that both see one decision).
 int conv_small_split(const ConvArgs& a) {
   if (a.gn_coef || conv_p4_plain_selected(a)) return 0;
-  if (g_conv1x1 && conv1x1_stream_ok(a)) {
-    const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
-    const int G = (g_num_cus / (8 * nTC)) * 8 * nTC;
-    if (G > 0 && (long long)nTP * nTC >= 4LL * G) return 0;
-  }
+  if (conv1x1_stream_grid(a)) return 0;
   const dim3 grid((a.M + CONV_BN - 1) / CONV_BN, (a.Cout + CONV_BM - 1) / CONV_BM);
   // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
   // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
@@ -4197,13 +4205,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   }
   if constexpr (sizeof(T) == 2) {
     // streaming 1x1 convs: >= 4 pixel tiles per persistent block (large pixel counts, N = 256)
-    if (g_conv1x1 && conv1x1_stream_ok(a)) {
-      const int nTC = a.Cout / CONV_BM, nTP = a.M / CONV_BN;
-      int G = (g_num_cus / (8 * nTC)) * 8 * nTC;  // whole XCD rounds of every cout tile
-      if (G > 0 && (long long)nTP * nTC >= 4LL * G) {
+    if (const int G = conv1x1_stream_grid(a)) {
+      {
         const int Cin = a.C1 + a.C2;
 #define ITSD_S1(NS)                                                                          \
-  if (Cin == 256) ITSD_LAUNCH((conv1x1_stream_kernel<256, NS>), dim3(G), dim3(256), 0, s, a);      \
+  if (Cin == 128) ITSD_LAUNCH((conv1x1_stream_kernel<128, NS>), dim3(G), dim3(256), 0, s, a);      \
+  else if (Cin == 256) ITSD_LAUNCH((conv1x1_stream_kernel<256, NS>), dim3(G), dim3(256), 0, s, a); \
   else if (Cin == 384) ITSD_LAUNCH((conv1x1_stream_kernel<384, NS>), dim3(G), dim3(256), 0, s, a); \
   else if (Cin == 512) ITSD_LAUNCH((conv1x1_stream_kernel<512, NS>), dim3(G), dim3(256), 0, s, a); \
   else ITSD_LAUNCH((conv1x1_stream_kernel<640, NS>), dim3(G), dim3(256), 0, s, a);
