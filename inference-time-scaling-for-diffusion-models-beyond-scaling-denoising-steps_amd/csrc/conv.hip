@@ -4131,7 +4131,8 @@ int conv_small_split(const ConvArgs& a) {
   // small levels: 64 x 64 tiles, whole K per block (auto: the 4x4 level and below, where
   // 128 x 128 tiles need split-K; measured slower than conv_pipe at 8x8)
   // (auto: not for K >= 7168 or Cout >= 1536, where the 128-tile pipe with split-K measured
-  // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt)
+  // 12-18 % faster at N = 256, profiles/r02_small_level_ab.txt; round 6: Cout >= 1536 only where the pipe's grid
+  // fills the chip -- the 4x4 q|k|v conv at N = 32 ran 48 pipe blocks without a K split)
   // Under ~one block per CU (the 2x2 / 1x1 levels, small batches) conv_small splits K itself
   // (in-launch combine), up to ~2 blocks per CU with >= 2 K-chunks a slice.
   const dim3 gs((a.M + SM_B - 1) / SM_B, (a.Cout + SM_B - 1) / SM_B);
@@ -4155,7 +4156,8 @@ int conv_small_split(const ConvArgs& a) {
   }
   if (g_small_conv && conv_small_ok(a) &&
       (g_small_conv == 2 || S > 1 || wide || small8 ||
-       (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 && !(a.splitk_ws && g_splitk && (a.K >= 7168 || a.Cout >= 1536))))) {
+       (a.Hout * a.Wout <= 16 && grid.x * grid.y < 1024 &&
+        !(a.splitk_ws && g_splitk && (a.K >= 7168 || (a.Cout >= 1536 && grid.x * grid.y >= 256)))))) {
     return S;
   }
   return 0;
