@@ -3988,14 +3988,15 @@ bool conv_p4_plain_selected(const ConvArgs& a) {
 
 // A sub-pixel phase conv on conv3x3_gn_p4_kernel<W, 128 | 256 x (ConvTranspose2d)>? subpix 1: the 2x2-tap
 // phases of a nearest-x2 upsample conv; subpix 2: the 3x3-tap phases of ConvTranspose2d(5, 2, 2, 1). W = the
-// input grid (8 / 16 / 32); auto where the 4 phases x 256-pixel tiles x 128-cout tiles fill the chip (>= 192)
+// input grid (8 / 16 / 32); auto from 64 tiles of 4 phases x 256 pixels x 128 couts (192 until round 6)
 bool conv_p4_sub_selected(const ConvArgs& a) {
   const int taps = a.subpix == 1 ? 4 : 9;
   if (!g_p4_sub || !a.subpix || !a.wfrag || a.ksize * a.ksize != taps || a.resid || a.vt_out || !a.zero ||
       a.gn_coef || a.Hout != a.Wout || !(a.Wout == 8 || a.Wout == 16 || a.Wout == 32) || a.Cout % CONV_BM ||
       a.C1 % 64 || a.C2 % 64 || a.C1 + a.C2 < 128 || a.K != taps * (a.C1 + a.C2) || a.M % GNW_BN)
     return false;
-  return 4LL * (a.M / GNW_BN) * (a.Cout / CONV_BM) >= 192;
+  // (round 6: from 64 tiles -- N = 32's 8x8 -> 16x16 upsample, 96 tiles, ran 43 us on split-K conv_pipe; was 192)
+  return 4LL * (a.M / GNW_BN) * (a.Cout / CONV_BM) >= 64;
 }
 
 // launch_conv's kernel choice for a fused GroupNorm conv: conv3x3_gn_p5_kernel?
