@@ -1432,6 +1432,12 @@ int itsd_set_option(const char* key, int value) {
     itsd::g_p5_pub = value;
     return ITSD_OK;
   }
+  if (!std::strcmp(key, "p5_xl")) {  // p5's split-K partials through one XCD's L2 (slices of a tile on one XCD): 0 off,
+                                     // 1 the shared combine at 8x8 / 16x16 (shipped), 2 every eligible form (A/B)
+    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_xl in [0,2]");
+    itsd::g_p5_xl = value;
+    return ITSD_OK;
+  }
   if (!std::strcmp(key, "p5_dist")) {  // p5's split-K combine shared by every slice (co-resident grids): 0 off (last arriver),
                                        // 1 on, 2 the same plans as 1 combined by the last arriver (bit-identity checks)
     if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_dist in [0,2]");

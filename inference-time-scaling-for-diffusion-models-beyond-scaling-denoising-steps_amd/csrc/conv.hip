@@ -66,6 +66,7 @@ int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's 
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_p5_sc = 1;         // the ResBlock's 1x1 shortcut folded into its block2 p5 conv: 0 off, 1 auto (cost model), 2 always
+int g_p5_xl = 1;    // p5's split-K partials exchanged through one XCD's L2 (ConvArgs::kxl): 0 off, 1 shipped forms, 2 all
 int g_p5_pub = 1;   // p5's two-slice last-arriver combine: only the first arriver stores its partial (0: both, round 5)
 int g_p5_dist = 1;       // p5's split-K combine shared by every slice of a tile where all items are co-resident (2: the
                          // same plans, combined by the last arriver)
@@ -2800,13 +2801,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
   const int bl = (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
   const int nit = bl < NI ? (NI - 1 - bl) / G + 1 : 0;
   if (nit == 0) return;  // (the host launches gridDim.x <= items)
-  // item k of this block -> pixel tile tp (fastest), K slice z, cout tile tc
+  // item k of this block -> pixel tile tp (fastest), K slice z, cout tile tc; XCD-local exchange (kxl): K slice
+  // fastest, so that a tile's slices are adjacent items on one XCD
+  const bool xl = a.kxl != 0;
+  const int d1 = xl ? ST : nTP, d2 = xl ? nTP : ST;  // the fastest index's extent, then the next one's
   auto item_of = [&](int k, int& tp, int& tc, int& z) {
     const int L = bl + k * G;
-    tp = L % nTP;
-    const int r = L / nTP;
-    z = r % ST;
-    tc = r / ST;
+    const int i1 = L % d1, r = L / d1, i2 = r % d2;
+    tp = xl ? i2 : i1;
+    z = xl ? i1 : i2;
+    tc = r / d2;
   };
   // chunk range [lo, hi) of slice z: the 3x3 conv's Cin / 64 chunks over slices 0 .. S-1, the shortcut's over S ..
   auto chunk_lo = [&](int z) { return z < S ? (nch * z) / S : (nchx * (z - S)) / S2; };
@@ -3018,16 +3022,33 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
         const uint32_t wbase = (uint32_t)(((size_t)tile * ST * 4 + wid) * NJW * 4096) + lane * 16;
         const uint32_t zstride = 4 * NJW * 4096;  // bytes between the slices of one (tile, wave)
         auto store_partial = [&]() __attribute__((always_inline)) {
+          if (xl) {  // (into this XCD's L2)
 #pragma unroll
-          for (int j = 0; j < NJW; ++j)
+            for (int j = 0; j < NJW; ++j)
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-              __builtin_amdgcn_raw_buffer_store_b128(
-                  u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]),
-                        __float_as_uint(acc[j][4 * g + 2]), __float_as_uint(acc[j][4 * g + 3])},
-                  slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
+              for (int g = 0; g < 4; ++g)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]),
+                          __float_as_uint(acc[j][4 * g + 2]), __float_as_uint(acc[j][4 * g + 3])},
+                    slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 0);
+          } else {  // (sc1: through to memory)
+#pragma unroll
+            for (int j = 0; j < NJW; ++j)
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{__float_as_uint(acc[j][4 * g]), __float_as_uint(acc[j][4 * g + 1]),
+                          __float_as_uint(acc[j][4 * g + 2]), __float_as_uint(acc[j][4 * g + 3])},
+                    slab, wbase + z * zstride + (j * 4 + g) * 1024, 0, 16);
+          }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         };
+        // a partial of this tile: sc0 (past L1, from this XCD's L2) under kxl, else sc1
+        auto load_partial = [&](uint32_t o) __attribute__((always_inline)) {
+          return xl ? __builtin_amdgcn_raw_buffer_load_b128(slab, o, 0, 1) : __builtin_amdgcn_raw_buffer_load_b128(slab, o, 0, 16);
+        };
+        // this wave's XCC_ID (HW_REG_XCC_ID bits 3:0): reported with the arrival under kxl
+        const int xcc = xl ? (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7) : 0;
         // (round 6) two slices, last-arriver form: arrival first; only the FIRST arriver stores its partial, the
         // last one adds it to its own from registers (p0 + p1 == p1 + p0 in IEEE arithmetic: bit-identical to the
         // slice-order sum). At N = 256's 4x4 level (256 items, S = 2) every block's combine runs at once and is
@@ -3052,6 +3073,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           constexpr int NJ = W == 4 ? 1 : W == 8 ? 2 : 4, NU = 16 / NJ;
           int* const tk = a.tickets + (tile * 4 + wid) * 32;  // (tiles x 4 x 32 <= kTicketCap: p5_dist)
           const int nown = z < NU ? (NU - 1 - z) / ST + 1 : 0;
+          if (xl && lane == 0) {  // this slice's XCD into the tile's mask (tk[1]) before its arrival
+            __hip_atomic_fetch_or(tk + 1, 1 << xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           if (nown == 0) {  // (ST > NU: no unit of its own) arrive and depart at once
             if (lane == 0) __hip_atomic_fetch_add(tk, 0x10001, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             TL(3);
@@ -3066,6 +3091,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
               v = __hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffff;
             }
             bad = v < ST;
+            if (xl && !bad) {  // every slice on this wave's XCD (else its partial is not in this L2)
+              const int msk = __hip_atomic_load(tk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              bad = msk != (1 << xcc);
+            }
             if (bad) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           bad = __builtin_amdgcn_readfirstlane(bad);
@@ -3112,11 +3141,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             u32x4 vv[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-              if (i < nl) vv[i] = __builtin_amdgcn_raw_buffer_load_b128(slab, slot_off(), 0, 16);
+              if (i < nl) vv[i] = load_partial(slot_off());
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               if (i < nl) *(u32x4*)(stg + i * 1024 + lane * 16) = vv[i];
-              if (i + 8 < nl) vv[i] = __builtin_amdgcn_raw_buffer_load_b128(slab, slot_off(), 0, 16);
+              if (i + 8 < nl) vv[i] = load_partial(slot_off());
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -3176,7 +3205,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           }
           if (lane == 0) {  // depart; the last one resets the counter
             const int old = __hip_atomic_fetch_add(tk, 0x10000, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((old >> 16) == ST - 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((old >> 16) == ST - 1) {
+              if (xl) __hip_atomic_store(tk + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
           TL(5);
           return;
@@ -3184,9 +3216,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
           // counter per (tile, wave): arrivals in bits 0-7, the last arriver's give-up in bit 8, the first arriver's
           // publication in bits 16+; whoever sees the other's final event resets it to 0 (the last arriver after the
           // publication, or the publisher after a give-up), so the counter is 0 between launches on every path
+          // (kxl: the arrival carries this slice's XCC_ID in bits 9-11; the last arriver compares the first's with its own)
           int* const tk = a.tickets + tile * 4 + wid;
           int old = 0;
-          if (lane == 0) old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) old = __hip_atomic_fetch_add(tk, 1 + (xcc << 9), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           old = __builtin_amdgcn_readfirstlane(old);
           if ((old & 0xff) == 0) {  // first: publish (R1: sc1 stores, drained, then the add) and go on
             store_partial();
@@ -3210,21 +3243,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_gn_p5_kernel(ConvArgs a) {
             bad = (v >> 16) == 0;  // (published meanwhile: the give-up's own return says so)
             if (bad) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xl && !bad && ((old >> 9) & 7) != xcc) {  // the publisher ran on another XCD: its partial is not here
+              bad = 1;
+              __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
           bad = __builtin_amdgcn_readfirstlane(bad);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+          auto add_other = [&](auto cp) __attribute__((always_inline)) {  // cp: the loads' cache policy
 #pragma unroll
-          for (int j = 0; j < NJW; ++j) {
-            u32x4 v[4];
+            for (int j = 0; j < NJW; ++j) {
+              u32x4 v[4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-              v[g] = __builtin_amdgcn_raw_buffer_load_b128(slab, wbase + (1 - z) * zstride + (j * 4 + g) * 1024, 0, 16);
+              for (int g = 0; g < 4; ++g)
+                v[g] = __builtin_amdgcn_raw_buffer_load_b128(slab, wbase + (1 - z) * zstride + (j * 4 + g) * 1024, 0,
+                                                             decltype(cp)::value);
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
+              for (int g = 0; g < 4; ++g)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[j][4 * g + e] += __uint_as_float(v[g][e]);
-            __builtin_amdgcn_sched_barrier(0);
-          }
+                for (int e = 0; e < 4; ++e) acc[j][4 * g + e] += __uint_as_float(v[g][e]);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          };
+          if (xl) add_other(std::integral_constant<int, 1>{});
+          else add_other(std::integral_constant<int, 16>{});
           if (bad) {
 #pragma unroll
             for (int j = 0; j < NJW; ++j)
@@ -4083,6 +4125,15 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   a.kdist = g_p5_dist == 1 && p.cb == 128 && p5_dist(tiles, p.s + p.s2, a.Wout);
   a.kpub = g_p5_pub;
   const dim3 g(std::min(items, g_num_cus));
+  {  // XCD-local exchange: the ST slices of a tile are adjacent items; every XCD's contiguous range of G / 8 blocks
+     // (and so of each item round) holds whole tiles when ST divides G / 8
+    const int ST = p.s + p.s2, G = (int)g.x;
+    // shipped (1): the shared combine at the 8x8 / 16x16 levels (N = 16 step -2.4 %, N = 32 -0.1..0.9 %); the other
+    // forms lose more to the slice-major order's weight re-reads than the L2 exchange saves (the 4x4 level and the
+    // two-slice form: N = 256 +1.1 %, profiles/r06/p5_xl_ops_r06as.txt) -- 2 takes every eligible form (A/B)
+    const bool form = g_p5_xl == 2 ? (a.kdist || (a.kpub && ST == 2)) : (a.kdist && a.Wout >= 8);
+    a.kxl = g_p5_xl && ST > 1 && form && G % 8 == 0 && (G / 8) % ST == 0;
+  }
   if (a.kdist) {  // (items <= CUs: 128-cout tiles at W <= 32)
     if (a.Wout == 32) ITSD_LAUNCH((conv3x3_gn_p5_kernel<32, 128, true>), g, dim3(512), 0, s, a);
     else if (a.Wout == 16) ITSD_LAUNCH((conv3x3_gn_p5_kernel<16, 128, true>), g, dim3(512), 0, s, a);

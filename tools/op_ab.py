@@ -15,7 +15,7 @@ from itsd import runtime as rt
 from itsd.arch import ARCH_A
 from itsd.model import UNet
 
-DEFAULTS = {"conv_dbg": 0, "attn_aq": 0, "attn_cs": 0, "small_conv": 1, "splitk": 1, "conv_variant": 2}
+DEFAULTS = {"p5_xl": 1, "splitk": 1}
 
 
 def main():

@@ -5,7 +5,8 @@ TL(slot): s_memrealtime, 100 MHz, one clock for every block). Never part of the 
 
 Per op: the launch's last repetition, every block's stamps relative to the earliest block entry (us):
 conv3x3_gn_p5_kernel -- MFMA wave 0: 0 entry, 1 after B0, 2 K loop done (last item), 3 split-K combined,
-4 epilogue done, 5 exit, 6 first chunk computed, 7 after its barrier; halo wave 4: 0 entry, 1 first item
+4 epilogue done, 5 exit (the shared-combine form <W, CB, true>: 3 partial stored + arrived, 4 every slice
+arrived, 5 combine and epilogue done), 6 first chunk computed, 7 after its barrier; halo wave 4: 0 entry, 1 first item
 opened (group statistics), 2 stage 0 emitted, 3 after B0, 4 stage 1 emitted, 6 after its barrier, 5 exit.
 """
 import argparse
@@ -75,9 +76,14 @@ def main():
         row("mfma chunk 0 computed", 0, 6)
         row("mfma chunk 0 barrier", 0, 7)
         row("mfma K loop done", 0, 2)
-        row("mfma split-K combined", 0, 3)
-        row("mfma epilogue done", 0, 4)
-        row("mfma exit", 0, 5)
+        if ", true>" in o["kernel"]:  # p5's shared combine (DIST): slots 3 / 4 / 5 mark its hand-off
+            row("mfma partial + arrived", 0, 3)
+            row("mfma all slices arrived", 0, 4)
+            row("mfma combine+epi done", 0, 5)
+        else:  # last-arriver / publish-once combine (a first arriver skips 3 and 4)
+            row("mfma split-K combined", 0, 3)
+            row("mfma epilogue done", 0, 4)
+            row("mfma exit", 0, 5)
         d_rt = (st[:, 0, 2] - st[:, 0, 1]).astype(np.float64)
         d_mt = (st[:, 1, 2] - st[:, 1, 1]).astype(np.float64)
         ok = (d_rt > 0) & (d_mt > 0)
