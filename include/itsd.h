@@ -179,7 +179,7 @@ int itsd_profile_op(itsd_unet* u, const float* x, const int32_t* t, int n, int o
 
 /* Process-wide choices between the shipped paths (api.hip lists every key and its range): kernel and tile
  * choices ("conv_variant", "splitk" 0/1, "splitk_inl", "small_conv", "gn_wide", "fuse_gn", "io_mfma", "p4_w",
- * "p4_sub", "p4_plain", "p4_c96", "p5", "p5_split", "p5_sc", "p5_pub", "p5_dist", "gn_fold", "attn_split", "attn_wide",
+ * "p4_sub", "p4_plain", "p4_c96", "p5", "p5_split", "p5_sc", "p5_pub", "p5_dist", "p5_xl", "gn_fold", "attn_split", "attn_wide",
  * "attn_wide_nq", "conv1x1" 0/1, "small_wide", "small_8x8", "subpix_split", "convt_prune"), the in-kernel hand-off
  * poll bound ("spin_bound"), and build-time choices read at create ("attn_fuse", "attn_s1", "tap_prune",
  * "down_merge"). Defaults are the shipped choices; every alternative is covered by a parity test. Measurement
