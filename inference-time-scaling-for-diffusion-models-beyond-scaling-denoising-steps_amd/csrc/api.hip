@@ -1433,8 +1433,9 @@ int itsd_set_option(const char* key, int value) {
     return ITSD_OK;
   }
   if (!std::strcmp(key, "p5_xl")) {  // p5's split-K partials through one XCD's L2 (slices of a tile on one XCD): 0 off,
-                                     // 1 the shared combine at 8x8 / 16x16 (shipped), 2 every eligible form (A/B)
-    if (value < 0 || value > 2) return fail(ITSD_ERR_INVALID, "p5_xl in [0,2]");
+                                     // 1 the shared combine at 8x8 / 16x16, 2 every eligible form (A/B), 3 (shipped)
+                                     // 1 + the two-slice form at 8x8 / 16x16 where K <= 3456
+    if (value < 0 || value > 3) return fail(ITSD_ERR_INVALID, "p5_xl in [0,3]");
     itsd::g_p5_xl = value;
     return ITSD_OK;
   }

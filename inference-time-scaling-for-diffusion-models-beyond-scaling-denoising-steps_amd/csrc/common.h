@@ -31,7 +31,7 @@ extern int g_p4_sub;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel
 extern int g_p5;            // small-level fused conv conv3x3_gn_p5_kernel: 0 off (W = 8), 1 auto, 2 forced (itsd_set_option "p5")
 extern int g_p5_split;      // its K slices: 0 auto (cost model), >= 1 forced (itsd_set_option "p5_split")
 extern int g_p5_sc;         // 1x1 shortcut folded into the block2 p5 conv: 0 off, 1 auto, 2 always ("p5_sc")
-extern int g_p5_xl;         // p5's split-K partials exchanged through one XCD's L2 (ConvArgs::kxl): 0 off, 1 shipped, 2 all ("p5_xl")
+extern int g_p5_xl;         // p5's split-K partials exchanged through one XCD's L2 (ConvArgs::kxl): 0 off, 1 / 2 / 3 (shipped) forms ("p5_xl")
 extern int g_p5_pub;        // p5's two-slice combine: only the first arriver stores its partial: 0 off, 1 on ("p5_pub")
 extern int g_p5_dist;       // p5 split-K combine by every slice where the grid is co-resident: 0 off, 1 on ("p5_dist")
 extern int g_p5_c64;        // 64-cout p5 items at the 8x8 / 4x4 levels: 0 off, 1 auto, 2 always ("p5_c64", diagnostic)

@@ -66,7 +66,8 @@ int g_p4_sub = 1;        // nearest-x2 upsample convs on conv3x3_gn_p4_kernel's 
 int g_p5 = 1;            // conv3x3_gn_p5_kernel at 8x8: 0 off, 1 auto (where p4 has < 192 tiles), 2 always (4x4: always)
 int g_p5_split = 0;      // its K slices: 0 auto, >= 1 forced
 int g_p5_sc = 1;         // the ResBlock's 1x1 shortcut folded into its block2 p5 conv: 0 off, 1 auto (cost model), 2 always
-int g_p5_xl = 1;    // p5's split-K partials exchanged through one XCD's L2 (ConvArgs::kxl): 0 off, 1 shipped forms, 2 all
+int g_p5_xl = 3;    // p5's split-K partials exchanged through one XCD's L2 (ConvArgs::kxl): 0 off, 1 the shared combine at
+                    // W >= 8, 2 every eligible form, 3 (shipped) 1 + the two-slice form at 8x8 / 16x16 where K <= 3456
 int g_p5_pub = 1;   // p5's two-slice last-arriver combine: only the first arriver stores its partial (0: both, round 5)
 int g_p5_dist = 1;       // p5's split-K combine shared by every slice of a tile where all items are co-resident (2: the
                          // same plans, combined by the last arriver)
@@ -4128,10 +4129,16 @@ static hipError_t launch_p5(const ConvArgs& a0, hipStream_t s) {
   {  // XCD-local exchange: the ST slices of a tile are adjacent items; every XCD's contiguous range of G / 8 blocks
      // (and so of each item round) holds whole tiles when ST divides G / 8
     const int ST = p.s + p.s2, G = (int)g.x;
-    // shipped (1): the shared combine at the 8x8 / 16x16 levels (N = 16 step -2.4 %, N = 32 -0.1..0.9 %); the other
-    // forms lose more to the slice-major order's weight re-reads than the L2 exchange saves (the 4x4 level and the
-    // two-slice form: N = 256 +1.1 %, profiles/r06/p5_xl_ops_r06as.txt) -- 2 takes every eligible form (A/B)
-    const bool form = g_p5_xl == 2 ? (a.kdist || (a.kpub && ST == 2)) : (a.kdist && a.Wout >= 8);
+    // 1: the shared combine at the 8x8 / 16x16 levels (N = 16 step -1.2..2.4 %, N = 32 -0.1..0.9 %); the other forms
+    // mostly lose more to the slice-major order's weight re-reads than the L2 exchange saves (the 4x4 level, the
+    // two-slice form at K >= 4608 and at 32x32: N = 256 +1.1 % with every form, profiles/r06/p5_xl_ops_r06as.txt);
+    // 2 takes every eligible form (A/B); 3 (shipped) adds the two-slice form where K <= 3456 at 8x8 / 16x16
+    // (N = 32 -1.0 % against 1, N = 16 / 64 / 256 equal: profiles/r06/stepab_p5_xl3_r06ax.txt)
+    // (3: K <= 3456 -- a cout tile's whole K of weights, <= 885 KB, per XCD)
+    const bool pub = a.kpub && ST == 2, dist8 = a.kdist && a.Wout >= 8;
+    const bool form = g_p5_xl == 2 ? (a.kdist || pub)
+                      : g_p5_xl == 3 ? (dist8 || (pub && (a.Wout == 8 || a.Wout == 16) && a.K <= 3456))
+                                     : dist8;
     a.kxl = g_p5_xl && ST > 1 && form && G % 8 == 0 && (G / 8) % ST == 0;
   }
   if (a.kdist) {  // (items <= CUs: 128-cout tiles at W <= 32)

@@ -21,7 +21,7 @@ from itsd.weights import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 REL_L2_BF16 = 2e-2
-_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1, "p5_sc": 1, "p5_pub": 1, "p5_xl": 1}
+_DEFAULTS = {"p5_dist": 1, "p5_split": 0, "p5": 1, "p5_sc": 1, "p5_pub": 1, "p5_xl": 3}
 
 
 def _rel_l2(a, b):
@@ -142,8 +142,9 @@ def test_two_slice_publish_once_bit_identical(n):
 def test_xcd_local_exchange_bit_identical(n):
     """(round 6, option p5_xl) The split-K partials exchanged through one XCD's L2 (a tile's slices as adjacent
     items, plain stores and L1-bypassing loads, each slice's XCC_ID checked with its arrival) against the
-    write-through exchange (p5_xl 0): bit for bit, for the shipped forms (1: the shared combine at 8x8 / 16x16) and
-    every eligible form (2: also the 4x4 level and the two-slice publish-once combine), auto plans and forced two /
+    write-through exchange (p5_xl 0): bit for bit, for the shared combine at 8x8 / 16x16 (1), every eligible form (2:
+    also the 4x4 level and the two-slice publish-once combine) and the shipped forms (3: 1 + the two-slice form at
+    8x8 / 16x16 where K <= 3456), auto plans and forced two /
     four slices at every p5 level; the status word stays 0 (no tile's slices ran on two XCDs)."""
     net = _net()
     x, t = _inputs(n, 6500 + n)
@@ -151,7 +152,7 @@ def test_xcd_local_exchange_bit_identical(n):
     for opts in ({}, {"p5": 2, "p5_split": 2, "p5_sc": 0}, {"p5": 2, "p5_split": 4, "p5_sc": 0}):
         ref = _eps(net, xd, td, p5_xl=0, **opts)
         assert torch.isfinite(ref).all()
-        for xl in (1, 2):
+        for xl in (1, 2, 3):
             out = _eps(net, xd, td, p5_xl=xl, **opts)
             assert torch.equal(out, ref), (opts, xl, _rel_l2(out, ref))
             assert net.native(n).query("status") == 0, (opts, xl)

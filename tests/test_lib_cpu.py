@@ -120,9 +120,9 @@ def test_conv_tile_options():
     for v in (0, 1):  # (round 6) p5's two-slice combine: both slices publish / only the first (shipped)
         rt.set_option("p5_pub", v)
     assert rt.lib().itsd_set_option(b"p5_pub", 2) != 0
-    for v in (0, 2, 1):  # (round 6) p5's split-K exchange through one XCD's L2: off / every form / shipped forms
+    for v in (0, 1, 2, 3):  # (round 6) p5's split-K exchange through one XCD's L2: off / shared combine / every form / shipped
         rt.set_option("p5_xl", v)
-    assert rt.lib().itsd_set_option(b"p5_xl", 3) != 0
+    assert rt.lib().itsd_set_option(b"p5_xl", 4) != 0
     for v in (0, 1):  # (round 6) conv_small's fused consumer GroupNorm: off / on (shipped)
         rt.set_option("small_gn", v)
     assert rt.lib().itsd_set_option(b"small_gn", 2) != 0

@@ -15,7 +15,7 @@ from itsd import runtime as rt
 from itsd.arch import ARCH_A
 from itsd.model import UNet
 
-DEFAULTS = {"p5_xl": 1, "splitk": 1}
+DEFAULTS = {"p5_xl": 3, "splitk": 1}
 
 
 def main():

@@ -22,7 +22,7 @@ from itsd.model import UNet
 DEFAULTS = {"gn_fold": 1, "p5": 1, "p5_split": 0, "p5_sc": 1, "splitk_inl": 1, "p4_plain": 1, "splitk": 1, "attn_split": 1,
             "p4_sub": 1, "gn_wide": 1, "small_conv": 1, "conv_variant": 2, "small_wide": 1, "small_8x8": 1,
             "subpix_split": 1, "conv1x1": 1, "attn_wide": 1, "attn_wide_nq": 1, "p4_w": 7, "convt_prune": 1, "small_minks": 8,
-            "attn_fuse": 1, "fuse_gn": 1, "conv_dbg": 0, "p4_xcd": 2, "spin_bound": 1 << 22, "p4_c96": 1, "p5_dist": 1, "p5_pub": 1, "small_gn": 1, "p5_xl": 1}
+            "attn_fuse": 1, "fuse_gn": 1, "conv_dbg": 0, "p4_xcd": 2, "spin_bound": 1 << 22, "p4_c96": 1, "p5_dist": 1, "p5_pub": 1, "small_gn": 1, "p5_xl": 3}
 
 
 def main():

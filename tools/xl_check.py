@@ -31,13 +31,13 @@ def main():
         x = torch.randn(n, 3, args.img, args.img, generator=g).cuda()
         t = torch.randint(0, a.T, (n,), generator=g).cuda()
         outs = []
-        for xl in (0, 1, 2, 0, 1, 2):
+        for xl in (0, 1, 2, 3, 0, 1, 2, 3):
             rt.set_option("p5_xl", xl)
             e = net(x, t)
             torch.cuda.synchronize()
             st = net.native(n).query("status")
             outs.append((e.clone(), st))
-        rt.set_option("p5_xl", 1)
+        rt.set_option("p5_xl", 3)
         same = all(torch.equal(outs[0][0], o[0]) for o in outs[1:])
         fin = all(bool(torch.isfinite(o[0]).all()) for o in outs)
         stat = [o[1] for o in outs]
